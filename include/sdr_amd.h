@@ -1,0 +1,131 @@
+/*
+ * sdr_amd.h -- C ABI of the MI355X-native FM/RDS DSP hot path (libsdr_amd.so, gfx950).
+ *
+ * Drop-in boundary for TheZxc07/real-time-SDR's per-block DSP (reference paths are relative to
+ * the reference repository root). Every entry point is extern "C", takes plain pointers and
+ * sizes, returns an int status (SDR_OK = 0) and enqueues work on the caller's HIP stream
+ * (`stream` = hipStream_t, NULL = default stream) without synchronising.
+ *
+ * Data layout (HBM): channel-major batches. A batch of nch independent I/Q streams is
+ * `[nch][len]` with a per-channel stride (in elements); per-channel state lives in device memory
+ * and is updated in place, exactly like the reference's by-reference state arguments.
+ *
+ * Numerics: the default ("exact") mode reproduces the reference's rounding points bit for bit:
+ * f32 products and sums in tap order without FMA (filter.cpp:111-115), f64 demod denominator
+ * and division (demod.cpp:17), f64 atan2/sin/cos rounded to f32 in the PLL (pll.cpp:39-52).
+ */
+#ifndef SDR_AMD_H
+#define SDR_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDR_OK 0
+#define SDR_E_INVALID (-1)   /* bad argument / shape */
+#define SDR_E_HIP (-2)       /* HIP runtime error (see sdr_last_error) */
+#define SDR_E_NOMEM (-3)
+#define SDR_E_NODEV (-4)     /* no gfx950 device */
+
+#define SDR_MAX_SYMS 256     /* symbols per block, >= n_rds/symbol_Fs + 1 for every mode */
+#define SDR_MAX_BITS 256
+
+/* Context flags */
+#define SDR_FLAG_FAST_FRONTEND 0x1  /* FMA front end: fm_demod within 1e-6 rel., not bit-exact */
+
+/* pllblock_args, include/pll.h:10-17 (same field order and types) */
+typedef struct sdr_pll_state {
+    float feedbackI;
+    float feedbackQ;
+    float integrator;
+    float phaseEst;
+    double trigOffset;
+    float lastCarrier;   /* the reference keeps it as pllOut[last]; out[0] of the next block */
+} sdr_pll_state;
+
+/* Static geometry of a context (mode table of project.cpp:67-108) */
+typedef struct sdr_info {
+    int nch, mode, rds_on;
+    int rf_Fs, rf_decim, if_Fs, audio_upsample, audio_decim, symbol_Fs, rf_taps;
+    int block_iq;   /* I/Q pairs per block (rffrontend.cpp:21)          mode 0: 73500 */
+    int block_if;   /* fm_demod samples per block                        mode 0: 7350  */
+    int n_audio;    /* audio frames per block (mono.cpp:28)             mode 0: 1470  */
+    int n_rds;      /* RDS baseband samples per block (rds.cpp:130)      mode 0: 2836  */
+    int history;    /* samples of history kept in front of each f32 stream */
+} sdr_info;
+
+typedef struct sdr_ctx sdr_ctx;
+
+const char *sdr_last_error(void);
+int sdr_version(void);
+
+/* ------------------------------------------------------------------ tap design (host, once)
+ * Same formulas, types and rounding as the reference; h must hold num_taps floats. */
+int sdr_impulse_response_lpf(float Fs, float Fc, unsigned short num_taps, float *h);            /* filter.cpp:13-29 */
+int sdr_impulse_response_lpf_gain(float Fs, float Fc, unsigned short num_taps, int u, float *h); /* filter.cpp:33-50 */
+int sdr_impulse_response_bpf(float Fs, const float *Fb, unsigned short num_taps, float *h);     /* filter.cpp:55-71 */
+int sdr_impulse_response_apf(float gain, unsigned short num_taps, float *h);                    /* filter.cpp:73-78 */
+int sdr_impulse_response_rrc(float Fs, unsigned short num_taps, float *h);                      /* filter.cpp:80-102 */
+
+/* ------------------------------------------------------------------ batched primitives
+ * All pointers are device pointers. `state` arrays are [nch][nstate] (nstate >= ntaps-1 for
+ * convolveFIR) and hold the previous block's last nstate inputs, zero-initialised by the caller
+ * like the reference's std::vector<float>(rf_taps-1). */
+
+/* convolveFIR(y, x, h, state, D): filter.cpp:106-121 (include/filter.h:20). y: [nch][nx/D]. */
+int sdr_convolve_fir(float *y, size_t y_stride, const float *x, size_t x_stride, int nch, int nx,
+                     const float *h, int ntaps, float *state, int nstate, int D, void *stream);
+/* convolveFIR(y, x, h, state, U, D): filter.cpp:123-147 (include/filter.h:24). y: [nch][nx*U/D].
+ * Phase restarts at 0 each block; only the last `nstate` (>= 100 for every mode) inputs of the
+ * previous block are kept (the reference copies ntaps-1, reading before x). */
+int sdr_convolve_fir_resample(float *y, size_t y_stride, const float *x, size_t x_stride, int nch, int nx,
+                              const float *h, int ntaps, float *state, int nstate, int U, int D, void *stream);
+/* fmDemodNoArctan(I, Q, prevI, prevQ, out): demod.cpp:3-24 (include/demod.h:5). prev: [nch][2]. */
+int sdr_fm_demod(float *out, size_t out_stride, const float *I, const float *Q, size_t iq_stride, int nch,
+                 int n, float *prev, void *stream);
+/* fmpll(in, freq, Fs, out, state, ncoScale, phaseAdjust, bw): pll.cpp:4-61 (include/pll.h:20).
+ * out: [nch][n+1]; out[ch][0] is set from state[ch].lastCarrier (the previous block's last
+ * sample, pll.cpp:18), state[ch].lastCarrier <- out[ch][n]. */
+int sdr_fmpll(float *out, size_t out_stride, const float *in, size_t in_stride, int nch, int n, float freq,
+              float Fs, sdr_pll_state *state, float ncoScale, float phaseAdjust, float normBandwidth,
+              void *stream);
+/* cdr(sps, signal): rds_utilities.cpp:4-21 (include/rds_utilities.h:6). offset: [nch] int32. */
+int sdr_cdr(int32_t *offset, const float *x, size_t x_stride, int nch, int n, int sps, void *stream);
+
+/* ------------------------------------------------------------------ fused pipeline
+ * A context owns the taps, every inter-stage buffer and all per-channel state of `nch`
+ * channels of one mode on one device: RF_frontend + mono + stereo + rds of the reference
+ * (rffrontend.cpp:9-77, mono.cpp:8-50, stereo.cpp:10-115, rds.cpp:11-193) as batched kernels. */
+int sdr_ctx_create(sdr_ctx **out, int device, int nch, int mode, int rds_on, int flags);
+int sdr_ctx_destroy(sdr_ctx *ctx);
+int sdr_ctx_reset(sdr_ctx *ctx, void *stream);      /* all state back to the reference's initial values */
+int sdr_ctx_info(const sdr_ctx *ctx, sdr_info *info);
+
+/* RF_frontend loop body (rffrontend.cpp:58-71): iq [nch][2*block_iq] u8 interleaved I/Q ->
+ * the context's fm_demod for this block. Advances the context to the next block. */
+int sdr_frontend(sdr_ctx *ctx, const uint8_t *iq, size_t iq_stride, void *stream);
+/* mono loop body (mono.cpp:34-42) on the current block: audio [nch][n_audio] int16 */
+int sdr_mono(sdr_ctx *ctx, int16_t *audio, size_t audio_stride, void *stream);
+/* stereo loop body (stereo.cpp:74-107): lr [nch][2*n_audio] int16, L/R interleaved */
+int sdr_stereo(sdr_ctx *ctx, int16_t *lr, size_t lr_stride, void *stream);
+/* rds DSP (rds.cpp:105-133): rds_clean [nch][n_rds] f32 (may be NULL: kept internally) */
+int sdr_rds_dsp(sdr_ctx *ctx, float *rds_clean, size_t rds_stride, void *stream);
+/* rds symbol/bit recovery (rds.cpp:135-167): per channel, for blocks with block_count > 5 and
+ * rds_on: offset = cdr(), symbols (0/1 bytes), bits (decoded 0/1 bytes). nbits[ch] = -1 on
+ * blocks that do not decode. Any output pointer may be NULL. Strides in elements. */
+int sdr_rds_bits(sdr_ctx *ctx, int32_t *offset, int32_t *nsym, uint8_t *symbols, size_t sym_stride,
+                 int32_t *nbits, uint8_t *bits, size_t bits_stride, void *stream);
+/* Copy out the context's current-block fm_demod [nch][block_if] (the reference's queue payload) */
+int sdr_get_fm_demod(sdr_ctx *ctx, float *fm, size_t fm_stride, void *stream);
+/* Debug / parity access to intermediates of the current block (device pointers into the
+ * context, valid until the next sdr_frontend): name in {"fm","pilot","carrier","band","rds_band",
+ * "gen_pilot","ipll","rds_dc","rds_filt","rds_clean","stereo_dc"}; *stride in elements. */
+int sdr_ctx_buffer(sdr_ctx *ctx, const char *name, const float **ptr, size_t *stride, int *len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1039 @@
+// sdr_kernels.hip -- MI355X (gfx950) kernels, launchers and C ABI of the FM/RDS DSP hot path.
+//
+// Hot path of TheZxc07/real-time-SDR recast as batched kernels over many independent channels:
+//   front end   u8 I/Q -> 101-tap FIR /10 on I and Q -> FM discriminator    rffrontend.cpp:58-71
+//   mono        101-tap resampler U/D -> int16                            mono.cpp:34-42
+//   stereo      pilot BPF -> PLL(19k, x2) ; band BPF ; mixer ; delay ; 2 resamplers -> L/R
+//                                                                          stereo.cpp:74-107
+//   rds DSP     BPF -> square -> BPF -> PLL(114k, x0.5) ; delay ; mixer -> 247/640 resampler
+//               -> RRC                                                     rds.cpp:105-133
+//   rds bits    cdr -> slicer -> Manchester -> differential               rds.cpp:135-167
+//
+// Numerics ("exact" mode, default): every kernel keeps the reference's rounding points --
+// f32 product then f32 add in tap order (no contraction: `fp contract(off)` below), the
+// discriminator's f64 denominator/division, the PLL's f64 atan2/sin/cos on f32 arguments.
+//
+// Layout: channel-major [nch][len]. Every f32 stream that a later FIR/resampler reads with
+// look-back is kept "extended": [2 parities][nch][HIST + len], the first HIST samples being the
+// previous block's last HIST samples, so a kernel reads x[-HIST..len) with no branch; the
+// producer of block b copies the history from the parity of block b-1.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <cstdarg>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sdr_amd.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int HIST = 160;        // history samples in front of every extended f32 stream (>= 150)
+constexpr int BLK = 256;         // threads per workgroup for the streaming kernels
+constexpr int FIR_TILE = 512;    // outputs per workgroup for the 101-tap FIRs
+constexpr int DEC_STATE = 8;     // ints of RDS decoder state per channel
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) return fail(SDR_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+#define LAUNCH_CHECK()                                                                              \
+    do {                                                                                            \
+        hipError_t e_ = hipGetLastError();                                                          \
+        if (e_ != hipSuccess) return fail(SDR_E_HIP, "launch failed at %s:%d: %s", __FILE__, __LINE__, \
+                                          hipGetErrorString(e_));                                   \
+    } while (0)
+
+// static_cast<short>(float) as g++/x86-64 lowers it (mono.cpp:41, stereo.cpp:101-102):
+// cvttss2si (INT_MIN when out of range or NaN), then the low 16 bits.
+__device__ __forceinline__ int32_t cvt_i32_x86(float v) {
+    return (v >= -2147483648.0f && v < 2147483648.0f) ? (int32_t)v : INT32_MIN;
+}
+__device__ __forceinline__ int16_t cvt_i16_x86(float v) {
+    return (int16_t)(uint16_t)((uint32_t)cvt_i32_x86(v) & 0xFFFFu);
+}
+
+// ------------------------------------------------------------------------------------------
+// Front end: u8 I/Q -> decimating FIR on I and Q -> discriminator (rffrontend.cpp:58-71,
+// filter.cpp:106-121, demod.cpp:3-24). Grid (tiles, nch). A tile computes decimated outputs
+// [c0, n1) (c0 = n0-1 so the discriminator has its previous sample) from an LDS window of
+// converted I/Q pairs, then writes fm_demod[n0, n1).
+// State: tail = last (ntaps-1) I/Q pairs of the previous block (u8, 128 == 0.0f),
+//        prev = last decimated (I, Q) of the previous block. Both double-buffered by parity.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLK) void k_frontend(
+    const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
+    uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
+    const float* __restrict__ h, int ntaps, int D, int block_iq, int block_if, int tile,
+    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride) {
+    extern __shared__ float4 smem4[];
+    const int ntaps_pad = (ntaps + 3) & ~3;
+    float* sh = reinterpret_cast<float*>(smem4);
+    const int ch = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int n0 = blockIdx.x * tile;
+    const int n1 = min(n0 + tile, block_if);
+    const int c0 = max(n0 - 1, 0);
+    const int m0 = c0 * D - (ntaps - 1);
+    const int m1 = (n1 - 1) * D;
+    const int W = m1 - m0 + 1;
+    float2* sx = reinterpret_cast<float2*>(sh + ntaps_pad);
+    float2* sds = sx + ((W + 1) & ~1);
+    const int hist_pairs = ntaps - 1;
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(iq + (size_t)ch * iq_stride);
+    const uint16_t* tin = reinterpret_cast<const uint16_t*>(tail_in + (size_t)ch * 2 * hist_pairs);
+
+    for (int i = tid; i < ntaps; i += BLK) sh[i] = h[i];
+    for (int i = tid; i < W; i += BLK) {
+        const int m = m0 + i;
+        const uint32_t pr = (m < 0) ? tin[hist_pairs + m] : src[m];
+        // float(((u - 128.0) / 128.0)) is exactly (u - 128) * 2^-7
+        sx[i] = make_float2(((float)(pr & 0xFFu) - 128.0f) * 0.0078125f, ((float)(pr >> 8) - 128.0f) * 0.0078125f);
+    }
+    __syncthreads();
+    for (int c = c0 + tid; c < n1; c += BLK) {
+        const int base = c * D - m0;
+        float aI = 0.0f, aQ = 0.0f;
+        for (int k = 0; k < ntaps; k++) {
+            const float hk = sh[k];
+            const float2 v = sx[base - k];
+            aI = aI + hk * v.x;
+            aQ = aQ + hk * v.y;
+        }
+        sds[c - c0] = make_float2(aI, aQ);
+    }
+    __syncthreads();
+    float* out = fm + (size_t)ch * fm_stride;
+    for (int n = n0 + tid; n < n1; n += BLK) {
+        const float2 cur = sds[n - c0];
+        const float2 pv = (n == 0) ? prev_in[ch] : sds[n - 1 - c0];
+        float r;
+        if ((cur.x == 0) & (cur.y == 0)) {
+            r = 0.0f;
+        } else {
+            const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
+            const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
+            r = (float)((double)num / den);
+        }
+        out[n] = r;
+    }
+    if (n1 == block_if && tid == 0) prev_out[ch] = sds[n1 - 1 - c0];
+    if (blockIdx.x == 0) {
+        const uint16_t* last = src + (block_iq - hist_pairs);
+        uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * hist_pairs);
+        for (int i = tid; i < hist_pairs; i += BLK) tout[i] = last[i];
+        const float* o = fm_other + (size_t)ch * fm_stride;
+        for (int i = tid; i < HIST; i += BLK) out[i - HIST] = o[block_if - HIST + i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Decimating FIR, filter.cpp:106-121: y[n] = sum_{k<ntaps} h[k] * x[nD-k], ascending k, f32
+// mul then add. x[m] for m < 0 comes from `hist` (hist[m], m >= -nhist). NT = 1 or 2 tap sets
+// sharing one staged window. SQUARE: the input is x*x (rds.cpp:111-113 fused into :116).
+// ------------------------------------------------------------------------------------------
+template <int NT, bool SQUARE>
+__global__ __launch_bounds__(BLK) void k_fir(const float* __restrict__ x, size_t x_stride,
+                                             const float* __restrict__ hist, size_t hist_stride,
+                                             const float* __restrict__ h0, const float* __restrict__ h1, int ntaps,
+                                             int D, int ny, int tile, float* __restrict__ y0,
+                                             float* __restrict__ y1, size_t y_stride) {
+    extern __shared__ float4 smem4[];
+    float* sh = reinterpret_cast<float*>(smem4);
+    const int ntaps_pad = (ntaps + 3) & ~3;
+    const int ch = blockIdx.y, tid = threadIdx.x;
+    const int n0 = blockIdx.x * tile, n1 = min(n0 + tile, ny);
+    const int m0 = n0 * D - (ntaps - 1), m1 = (n1 - 1) * D;
+    const int W = m1 - m0 + 1;
+    float* sx = sh + NT * ntaps_pad;
+    const float* xc = x + (size_t)ch * x_stride;
+    const float* hc = hist + (size_t)ch * hist_stride;
+    for (int i = tid; i < ntaps; i += BLK) {
+        sh[i] = h0[i];
+        if (NT == 2) sh[ntaps_pad + i] = h1[i];
+    }
+    for (int i = tid; i < W; i += BLK) {
+        const int m = m0 + i;
+        float v = (m < 0) ? hc[m] : xc[m];
+        if (SQUARE) v = v * v;
+        sx[i] = v;
+    }
+    __syncthreads();
+    for (int n = n0 + tid; n < n1; n += BLK) {
+        const int base = n * D - m0;
+        float a0 = 0.0f, a1 = 0.0f;
+        for (int k = 0; k < ntaps; k++) {
+            const float v = sx[base - k];
+            a0 = a0 + sh[k] * v;
+            if (NT == 2) a1 = a1 + sh[ntaps_pad + k] * v;
+        }
+        y0[(size_t)ch * y_stride + n] = a0;
+        if (NT == 2) y1[(size_t)ch * y_stride + n] = a1;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Rational resampler, filter.cpp:123-147. Output n: phase = nD mod U, q = (nD - phase)/U,
+// y[n] = sum_j hp[phase][j] * x[q - j] (j ascending == k ascending), hp = polyphase taps,
+// cnt[phase] = number of taps of that phase. The phase restarts every block (the reference
+// recomputes it from n, :131). OUT: 0 -> f32 y, 1 -> int16(16384*y) (mono.cpp:40-42),
+// 2 -> stereo L/R int16 from two inputs a (mono) and b (stereo) (stereo.cpp:100-107).
+// ------------------------------------------------------------------------------------------
+template <int OUT>
+__global__ __launch_bounds__(BLK) void k_resample(const float* __restrict__ xa, const float* __restrict__ ha,
+                                                  size_t xa_stride, size_t ha_stride,
+                                                  const float* __restrict__ xb, const float* __restrict__ hb,
+                                                  size_t xb_stride, size_t hb_stride,
+                                                  const float* __restrict__ hp, const int* __restrict__ cnt,
+                                                  int L, int U, int D, int ny, int tile, int hist_lo,
+                                                  void* __restrict__ y, size_t y_stride) {
+    extern __shared__ float4 smem4[];
+    float* sa = reinterpret_cast<float*>(smem4);
+    const int ch = blockIdx.y, tid = threadIdx.x;
+    const int n0 = blockIdx.x * tile, n1 = min(n0 + tile, ny);
+    const int qlo = (int)(((long long)n0 * D) / U) - L;   // smallest input index any output reads
+    const int qhi = (int)(((long long)(n1 - 1) * D) / U);
+    const int W = qhi - qlo + 1;
+    const int Wp = (W + 3) & ~3;
+    float* sb = sa + Wp;
+    {
+        const float* xc = xa + (size_t)ch * xa_stride;
+        const float* hc = ha + (size_t)ch * ha_stride;
+        for (int i = tid; i < W; i += BLK) {
+            const int m = qlo + i;
+            sa[i] = (m < 0) ? (m >= hist_lo ? hc[m] : 0.0f) : xc[m];
+        }
+    }
+    if (OUT == 2) {
+        const float* xc = xb + (size_t)ch * xb_stride;
+        const float* hc = hb + (size_t)ch * hb_stride;
+        for (int i = tid; i < W; i += BLK) {
+            const int m = qlo + i;
+            sb[i] = (m < 0) ? (m >= hist_lo ? hc[m] : 0.0f) : xc[m];
+        }
+    }
+    __syncthreads();
+    for (int n = n0 + tid; n < n1; n += BLK) {
+        const long long nd = (long long)n * D;
+        const int ph = (int)(nd % U);
+        const int q = (int)(nd / U);
+        const float* hr = hp + (size_t)ph * L;
+        const int c = cnt[ph];
+        const int base = q - qlo;
+        float a = 0.0f, b = 0.0f;
+        for (int j = 0; j < c; j++) {
+            const float hj = hr[j];
+            a = a + hj * sa[base - j];
+            if (OUT == 2) b = b + hj * sb[base - j];
+        }
+        if (OUT == 0) {
+            static_cast<float*>(y)[(size_t)ch * y_stride + n] = a;
+        } else if (OUT == 1) {
+            static_cast<int16_t*>(y)[(size_t)ch * y_stride + n] = cvt_i16_x86(16384 * a);
+        } else {
+            int16_t* o = static_cast<int16_t*>(y) + (size_t)ch * y_stride + 2 * n;
+            o[0] = cvt_i16_x86(16384 * (a + b));   // left  = 16384*(m + s)
+            o[1] = cvt_i16_x86(16384 * (a - b));   // right = 16384*(m - s)
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// PLL / NCO, pll.cpp:4-61: one lane per channel, the recurrence is serial in time.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_pll(const float* __restrict__ in, size_t in_stride, int n, int nch,
+                                            float freq, float Fs, float* __restrict__ out, size_t out_stride,
+                                            sdr_pll_state* __restrict__ st, float ncoScale, float phaseAdjust,
+                                            float normBandwidth) {
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= nch) return;
+    const float Cp = 2.666;
+    const float Ci = 3.555;
+    const float Kp = normBandwidth * Cp;
+    const float Ki = normBandwidth * normBandwidth * Ci;
+    const double w = 2 * 3.14159265358979323846 * (freq / Fs);  // 2*PI*(freq/Fs), pll.cpp:47
+    sdr_pll_state s = st[ch];
+    const float* x = in + (size_t)ch * in_stride;
+    float* o = out + (size_t)ch * out_stride;
+    o[0] = s.lastCarrier;
+    float fbI = s.feedbackI, fbQ = s.feedbackQ, integ = s.integrator, ph = s.phaseEst;
+    double toff = s.trigOffset;
+    float last = s.lastCarrier;
+    for (int i = 0; i < n; i++) {
+        const float xi = x[i];
+        const float eI = xi * fbI;
+        const float eQ = xi * (-fbQ);
+        const float e = (float)atan2((double)eQ, (double)eI);
+        integ = integ + Ki * e;
+        ph = ph + Kp * e + integ;
+        toff += 1.0;
+        const float t = (float)(w * toff + (double)ph);
+        double sv, cv;
+        sincos((double)t, &sv, &cv);
+        fbI = (float)cv;
+        fbQ = (float)sv;
+        last = (float)cos((double)(t * ncoScale + phaseAdjust));
+        o[i + 1] = last;
+    }
+    s.feedbackI = fbI;
+    s.feedbackQ = fbQ;
+    s.integrator = integ;
+    s.phaseEst = ph;
+    s.trigOffset = toff;
+    s.lastCarrier = last;
+    st[ch] = s;
+}
+
+// ------------------------------------------------------------------------------------------
+// Mixers. stereo.cpp:83-85: stereo_dc = 2.0*band*carrier (f64 product, one rounding).
+// rds.cpp:125-127: rds_dc = (2*delay)*ipll with delay[i] = rds_band[i-50] (the 101-tap APF of
+// filter.cpp:73-78 is an exact 50-sample delay for finite inputs). Also copies the history.
+// ------------------------------------------------------------------------------------------
+template <bool RDS>
+__global__ __launch_bounds__(BLK) void k_mix(const float* __restrict__ a, size_t a_stride,
+                                             const float* __restrict__ c, size_t c_stride, int n,
+                                             float* __restrict__ y, const float* __restrict__ y_other,
+                                             size_t y_stride, int delay) {
+    const int ch = blockIdx.y;
+    const int i = blockIdx.x * BLK + threadIdx.x;
+    const float* ac = a + (size_t)ch * a_stride;
+    const float* cc = c + (size_t)ch * c_stride;
+    float* yc = y + (size_t)ch * y_stride;
+    if (i < n) {
+        if (RDS) {
+            const float d = ac[i - delay] + 0.0f;   // + 0.0f: the APF sum turns -0 into +0
+            yc[i] = 2 * d * cc[i];
+        } else {
+            yc[i] = (float)(2.0 * (double)ac[i] * (double)cc[i]);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < HIST) {
+        yc[(int)threadIdx.x - HIST] = y_other[(size_t)ch * y_stride + n - HIST + threadIdx.x];
+    }
+}
+
+// copy the previous parity's last HIST samples in front of this parity's stream
+__global__ void k_hist_copy(float* __restrict__ y, const float* __restrict__ y_other, size_t stride, int n) {
+    const int ch = blockIdx.x;
+    for (int i = threadIdx.x; i < HIST; i += blockDim.x)
+        y[(size_t)ch * stride + i - HIST] = y_other[(size_t)ch * stride + n - HIST + i];
+}
+
+// state <- last nstate of x (filter.cpp:119 / :145) for the primitive entry points
+__global__ void k_state_update(float* __restrict__ state, int nstate, const float* __restrict__ x,
+                               size_t x_stride, int nx) {
+    const int ch = blockIdx.x;
+    float* s = state + (size_t)ch * nstate;
+    const float* xc = x + (size_t)ch * x_stride;
+    if (nx >= nstate) {
+        for (int i = threadIdx.x; i < nstate; i += blockDim.x) s[i] = xc[nx - nstate + i];
+    } else {
+        // shift (single workgroup per channel: read all, barrier, write)
+        for (int base = 0; base < nstate; base += blockDim.x) {
+            const int i = base + threadIdx.x;
+            float v = 0.0f;
+            if (i < nstate) v = (i + nx < nstate) ? s[i + nx] : xc[i + nx - nstate];
+            __syncthreads();
+            if (i < nstate) s[i] = v;
+            __syncthreads();
+        }
+    }
+}
+
+// fmDemodNoArctan over separate I/Q arrays (demod.cpp:3-24); prev updated by k_demod_prev.
+__global__ __launch_bounds__(BLK) void k_demod(float* __restrict__ out, size_t out_stride,
+                                               const float* __restrict__ I, const float* __restrict__ Q,
+                                               size_t iq_stride, int n, const float2* __restrict__ prev) {
+    const int ch = blockIdx.y;
+    const int i = blockIdx.x * BLK + threadIdx.x;
+    if (i >= n) return;
+    const float* Ic = I + (size_t)ch * iq_stride;
+    const float* Qc = Q + (size_t)ch * iq_stride;
+    const float ci = Ic[i], cq = Qc[i];
+    const float2 pv = (i == 0) ? prev[ch] : make_float2(Ic[i - 1], Qc[i - 1]);
+    float r;
+    if ((ci == 0) & (cq == 0)) {
+        r = 0.0f;
+    } else {
+        const float num = ci * (cq - pv.y) - cq * (ci - pv.x);
+        const double den = (double)ci * (double)ci + (double)cq * (double)cq;
+        r = (float)((double)num / den);
+    }
+    out[(size_t)ch * out_stride + i] = r;
+}
+
+__global__ void k_demod_prev(float2* __restrict__ prev, const float* __restrict__ I, const float* __restrict__ Q,
+                             size_t iq_stride, int n, int nch) {
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch < nch) prev[ch] = make_float2(I[(size_t)ch * iq_stride + n - 1], Q[(size_t)ch * iq_stride + n - 1]);
+}
+
+// cdr(), rds_utilities.cpp:4-21: argmax over offsets i < sps of sum_k |(int)x[k*sps+i]|,
+// first maximum wins, 0 when every sum is 0. One wave per channel, one lane per offset.
+__device__ __forceinline__ int cdr_wave(const float* x, int n, int sps, int* sums) {
+    const int lane = threadIdx.x;
+    const int nk = n / sps;
+    for (int i = lane; i < sps; i += blockDim.x) {
+        uint32_t s = 0;
+        for (int k = 0; k < nk; k++) {
+            const int32_t v = cvt_i32_x86(x[k * sps + i]);
+            s += (uint32_t)(v < 0 ? -(uint32_t)v : (uint32_t)v);
+        }
+        sums[i] = (int32_t)s;
+    }
+    __syncthreads();
+    int maxi = 0, maxv = 0;
+    for (int i = 0; i < sps; i++) {
+        if (sums[i] > maxv) {
+            maxv = sums[i];
+            maxi = i;
+        }
+    }
+    return maxi;
+}
+
+__global__ __launch_bounds__(64) void k_cdr(int32_t* __restrict__ offset, const float* __restrict__ x,
+                                            size_t x_stride, int n, int sps) {
+    extern __shared__ int sums_dyn[];
+    const int ch = blockIdx.x;
+    const int off = cdr_wave(x + (size_t)ch * x_stride, n, sps, sums_dyn);
+    if (threadIdx.x == 0) offset[ch] = off;
+}
+
+// RDS symbol and bit recovery for one block (rds.cpp:135-167): cdr, slicer (:157-161),
+// manchester_decode (rds_utilities.cpp:34-68), differential_decode (:70-88).
+// dec[ch*8 + {0..4}] = block_count, half_symbol, start, last_bit, sample_offset.
+__global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, size_t x_stride, int n, int sps,
+                                                 int rds_on, int32_t* __restrict__ dec,
+                                                 int32_t* __restrict__ offset_out, int32_t* __restrict__ nsym_out,
+                                                 uint8_t* __restrict__ sym_out, size_t sym_stride,
+                                                 int32_t* __restrict__ nbits_out, uint8_t* __restrict__ bits_out,
+                                                 size_t bits_stride) {
+    extern __shared__ int sums_dyn[];
+    __shared__ uint8_t symbols[SDR_MAX_SYMS];
+    const int ch = blockIdx.x;
+    const int lane = threadIdx.x;
+    int32_t* d = dec + (size_t)ch * DEC_STATE;
+    const int block_count = d[0];
+    const float* xc = x + (size_t)ch * x_stride;
+    const bool decode = (block_count > 5) && rds_on;
+    if (!decode) {
+        if (lane == 0) {
+            if (offset_out) offset_out[ch] = d[4];
+            if (nsym_out) nsym_out[ch] = 0;
+            if (nbits_out) nbits_out[ch] = -1;
+            d[0] = block_count + 1;
+        }
+        return;
+    }
+    const int off = cdr_wave(xc, n, sps, sums_dyn);
+    int m = 0;
+    if (off < n) m = (n - off + sps - 1) / sps;     // i with off + i*sps < n
+    if (m > SDR_MAX_SYMS) m = SDR_MAX_SYMS;
+    for (int i = lane; i < m; i += blockDim.x) symbols[i] = xc[off + i * sps] > 0;
+    __syncthreads();
+    if (lane == 0) {
+        int half_symbol = d[1], start = d[2], last_bit = d[3];
+        uint8_t bits[SDR_MAX_BITS];
+        int nb = 0;
+        if (start) bits[nb++] = (uint8_t)half_symbol;
+        if (block_count == 0) {  // dead in the reference (decoding starts at block 6), kept for parity
+            int score = 0;
+            for (int i = 0; i < m - 1; i += 2) score += symbols[i] ^ symbols[i + 1];
+            for (int j = 1; j < m - 1; j += 2) score -= symbols[j] ^ symbols[j + 1];
+            start = score < 0;
+        }
+        for (int i = start; i < m - 1 && nb < SDR_MAX_BITS; i += 2) bits[nb++] = symbols[i];
+        if (((m - start) & 0x01) == 1) {
+            half_symbol = symbols[m - 1];
+            start = 1;
+        } else {
+            start = 0;
+        }
+        uint8_t* bo = bits_out ? bits_out + (size_t)ch * bits_stride : nullptr;
+        if (nb > 0) {
+            uint8_t prevb = bits[0];
+            const uint8_t first = (block_count == 0) ? bits[0] : (uint8_t)(bits[0] ^ (uint8_t)last_bit);
+            if (bo) bo[0] = first;
+            for (int i = 1; i < nb; i++) {
+                if (bo) bo[i] = bits[i] ^ prevb;
+                prevb = bits[i];
+            }
+            last_bit = bits[nb - 1];
+        }
+        if (sym_out) {
+            uint8_t* so = sym_out + (size_t)ch * sym_stride;
+            for (int i = 0; i < m; i++) so[i] = symbols[i];
+        }
+        d[1] = half_symbol;
+        d[2] = start;
+        d[3] = last_bit;
+        d[4] = off;
+        d[0] = block_count + 1;
+        if (offset_out) offset_out[ch] = off;
+        if (nsym_out) nsym_out[ch] = m;
+        if (nbits_out) nbits_out[ch] = nb;
+    }
+}
+
+__global__ void k_fill_u8(uint8_t* p, uint8_t v, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
+
+size_t fir_lds_bytes(int ntaps, int nt, int tile, int D) {
+    const int ntaps_pad = (ntaps + 3) & ~3;
+    const int W = (tile - 1) * D + ntaps;
+    return (size_t)(nt * ntaps_pad + W + 4) * sizeof(float);
+}
+
+size_t frontend_lds_bytes(int ntaps, int tile, int D) {
+    const int ntaps_pad = (ntaps + 3) & ~3;
+    const int W = tile * D + ntaps;                  // window incl. the extra output at n0-1
+    return (size_t)ntaps_pad * 4 + (size_t)((W + 1) & ~1) * 8 + (size_t)(tile + 1) * 8 + 64;
+}
+
+size_t resample_lds_bytes(int L, int U, int D, int tile, int ninputs) {
+    const int W = (int)(((long long)tile * D) / U) + L + 2;
+    return (size_t)ninputs * ((W + 3) & ~3) * sizeof(float) + 64;
+}
+
+// polyphase tap table: row p holds h[p], h[p+U], ... (cnt[p] entries), rows padded to L
+struct Polyphase {
+    std::vector<float> table;
+    std::vector<int> cnt;
+    int L = 0;
+};
+
+Polyphase make_polyphase(const std::vector<float>& h, int U) {
+    Polyphase p;
+    const int ntaps = (int)h.size();
+    int maxc = 0;
+    p.cnt.resize(U);
+    for (int ph = 0; ph < U; ph++) {
+        p.cnt[ph] = ph < ntaps ? (ntaps - ph + U - 1) / U : 0;
+        maxc = std::max(maxc, p.cnt[ph]);
+    }
+    p.L = (maxc + 3) & ~3;
+    p.table.assign((size_t)U * p.L, 0.0f);
+    for (int ph = 0; ph < U; ph++)
+        for (int j = 0; j < p.cnt[ph]; j++) p.table[(size_t)ph * p.L + j] = h[ph + (size_t)U * j];
+    return p;
+}
+
+}  // namespace
+
+// ============================================================================================
+// Context
+// ============================================================================================
+struct sdr_ctx {
+    int device = 0, nch = 0, mode = 0, rds_on = 0, flags = 0;
+    sdr_info info{};
+    int ntaps = 101;
+    // taps (device)
+    float *rf_h = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
+          *rrc_h = nullptr;
+    float *audio_pp = nullptr, *rdsbb_pp = nullptr;   // polyphase tables
+    int *audio_cnt = nullptr, *rdsbb_cnt = nullptr;
+    int audio_L = 0, rdsbb_L = 0;
+    // extended streams [2][nch][HIST + len]; pointers below are the data bases of parity 0
+    float *fm = nullptr, *sdc = nullptr, *rband = nullptr, *rdc = nullptr, *rfilt = nullptr;
+    size_t fm_stride = 0, rf_stride = 0;               // per-channel strides (if, rds lengths)
+    size_t fm_par = 0, rf_par = 0;                      // parity offsets in elements
+    // plain per-block buffers
+    float *pilot = nullptr, *band = nullptr, *gpilot = nullptr, *carrier = nullptr, *ipll = nullptr,
+          *rds_clean = nullptr;
+    size_t plain_stride = 0, pll_stride = 0, clean_stride = 0;
+    // state
+    uint8_t* tail = nullptr;                            // [2][nch][2*(ntaps-1)]
+    float2* prev = nullptr;                             // [2][nch]
+    sdr_pll_state *st_pll = nullptr, *rds_pll = nullptr;
+    int32_t* dec = nullptr;                             // [nch][DEC_STATE]
+    int parity = 1;                                     // parity of the current block
+    long long block = -1;                               // index of the current block
+    long long stereo_done = -1, rds_dsp_done = -1, rds_bits_done = -1, mono_done = -1;
+    std::vector<void*> allocs;
+
+    float* fm_cur() const { return fm + parity * fm_par; }
+    float* fm_oth() const { return fm + (parity ^ 1) * fm_par; }
+    float* ext(float* base, size_t par, int p) const { return base + p * par; }
+};
+
+namespace {
+
+template <typename T>
+int dalloc(sdr_ctx* c, T** p, size_t count) {
+    void* v = nullptr;
+    HIP_TRY(hipMalloc(&v, count * sizeof(T) + 256));
+    HIP_TRY(hipMemset(v, 0, count * sizeof(T) + 256));
+    c->allocs.push_back(v);
+    *p = static_cast<T*>(v);
+    return SDR_OK;
+}
+
+template <typename T>
+int upload(sdr_ctx* c, T** p, const std::vector<T>& host) {
+    int r = dalloc(c, p, host.size());
+    if (r) return r;
+    HIP_TRY(hipMemcpy(*p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SDR_OK;
+}
+
+int fill_info(sdr_info* in, int nch, int mode, int rds_on) {
+    std::memset(in, 0, sizeof(*in));
+    in->nch = nch;
+    in->mode = mode;
+    in->rds_on = rds_on;
+    in->rf_taps = 101;
+    in->rf_Fs = 2400000; in->rf_decim = 10; in->if_Fs = 240000; in->audio_upsample = 1;
+    in->audio_decim = 5; in->symbol_Fs = 39;
+    switch (mode) {  // project.cpp:67-108
+        case 0: break;
+        case 1: in->rf_Fs = 1440000; in->rf_decim = 4; in->audio_decim = 9; in->if_Fs = 360000; break;
+        case 2: in->audio_decim = 800; in->audio_upsample = 147; in->symbol_Fs = 20; break;
+        case 3: in->rf_Fs = 1152000; in->rf_decim = 3; in->audio_decim = 1280; in->if_Fs = 384000;
+                in->audio_upsample = 147; in->symbol_Fs = 20; break;
+        default: return fail(SDR_E_INVALID, "mode %d not in 0..3", mode);
+    }
+    const int U = in->audio_upsample, D = in->audio_decim;
+    in->block_iq = (1470 * in->rf_decim * D) / U;
+    in->block_if = (1470 * D) / U;
+    in->n_audio = in->block_if * U / D;
+    in->n_rds = in->block_if * 247 / 640;
+    in->history = HIST;
+    return SDR_OK;
+}
+
+int init_state(sdr_ctx* c, hipStream_t s) {
+    const sdr_info& in = c->info;
+    // every buffer back to zero (the reference's value-initialised vectors)
+    HIP_TRY(hipMemsetAsync(c->fm - HIST, 0, 2 * c->fm_par * sizeof(float), s));
+    HIP_TRY(hipMemsetAsync(c->sdc - HIST, 0, 2 * c->fm_par * sizeof(float), s));
+    HIP_TRY(hipMemsetAsync(c->rband - HIST, 0, 2 * c->fm_par * sizeof(float), s));
+    HIP_TRY(hipMemsetAsync(c->rdc - HIST, 0, 2 * c->fm_par * sizeof(float), s));
+    HIP_TRY(hipMemsetAsync(c->rfilt - HIST, 0, 2 * c->rf_par * sizeof(float), s));
+    const size_t tail_bytes = (size_t)2 * c->nch * 2 * (c->ntaps - 1);
+    hipLaunchKernelGGL(k_fill_u8, dim3((unsigned)((tail_bytes + 255) / 256)), dim3(256), 0, s, c->tail,
+                       (uint8_t)128, tail_bytes);  // u8 128 == 0.0f: zero FIR state
+    LAUNCH_CHECK();
+    HIP_TRY(hipMemsetAsync(c->prev, 0, (size_t)2 * c->nch * sizeof(float2), s));
+    std::vector<sdr_pll_state> st(c->nch);
+    for (auto& p : st) p = sdr_pll_state{1.0f, 0.0f, 0.0f, 0.0f, 0.0, 1.0f};  // stereo.cpp:51-57, :45
+    HIP_TRY(hipMemcpyAsync(c->st_pll, st.data(), st.size() * sizeof(sdr_pll_state), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->rds_pll, st.data(), st.size() * sizeof(sdr_pll_state), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(c->dec, 0, (size_t)c->nch * DEC_STATE * sizeof(int32_t), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->parity = 1;
+    c->block = -1;
+    c->stereo_done = c->rds_dsp_done = c->rds_bits_done = c->mono_done = -1;
+    (void)in;
+    return SDR_OK;
+}
+
+inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+}  // namespace
+
+extern "C" {
+
+const char* sdr_last_error(void) { return g_err.c_str(); }
+int sdr_version(void) { return 1; }
+
+int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int flags) {
+    if (!out || nch <= 0) return fail(SDR_E_INVALID, "bad arguments");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0)
+        return fail(SDR_E_NODEV, "no HIP device %d", device);
+    HIP_TRY(hipSetDevice(device));
+    sdr_ctx* c = new sdr_ctx();
+    c->device = device;
+    c->nch = nch;
+    c->mode = mode;
+    c->rds_on = rds_on ? 1 : 0;
+    c->flags = flags;
+    int r = fill_info(&c->info, nch, mode, c->rds_on);
+    if (r) { delete c; return r; }
+    const sdr_info& in = c->info;
+    const int T = in.rf_taps, U = in.audio_upsample;
+    c->ntaps = T;
+    // ---- taps (host design, reference formulas) ----
+    std::vector<float> rf(T), audio((size_t)T * U), pilot(T), stereo(T), rds(T), rds_sq(T), rdsbb((size_t)T * 247),
+        rrc(T);
+    const float fb_pilot[2] = {18.5e3f, 19.5e3f}, fb_stereo[2] = {22e3f, 54e3f};
+    const float fb_rds[2] = {54e3f, 60e3f}, fb_rds_sq[2] = {113.5e3f, 114.5e3f};
+    sdr_impulse_response_lpf((float)in.rf_Fs, 100000.0f, (unsigned short)T, rf.data());                  // rffrontend.cpp:24
+    sdr_impulse_response_lpf_gain((float)(in.if_Fs * U), 16000.0f, (unsigned short)(T * U), U, audio.data()); // mono.cpp:22
+    sdr_impulse_response_bpf((float)(in.rf_Fs / in.rf_decim), fb_pilot, (unsigned short)T, pilot.data());  // stereo.cpp:65
+    sdr_impulse_response_bpf((float)(in.rf_Fs / in.rf_decim), fb_stereo, (unsigned short)T, stereo.data()); // stereo.cpp:67
+    sdr_impulse_response_lpf_gain((float)(in.if_Fs * 247), 3e3f, (unsigned short)(T * 247), 247, rdsbb.data()); // rds.cpp:61
+    sdr_impulse_response_bpf((float)in.if_Fs, fb_rds, (unsigned short)T, rds.data());                      // rds.cpp:62
+    sdr_impulse_response_bpf((float)in.if_Fs, fb_rds_sq, (unsigned short)T, rds_sq.data());                // rds.cpp:63
+    sdr_impulse_response_rrc((float)(2375 * in.symbol_Fs), (unsigned short)T, rrc.data());                 // rds.cpp:65
+    Polyphase pa = make_polyphase(audio, U), pr = make_polyphase(rdsbb, 247);
+    c->audio_L = pa.L;
+    c->rdsbb_L = pr.L;
+#define TRY(x) do { int r_ = (x); if (r_) { sdr_ctx_destroy(c); return r_; } } while (0)
+    TRY(upload(c, &c->rf_h, rf));
+    TRY(upload(c, &c->pilot_h, pilot));
+    TRY(upload(c, &c->stereo_h, stereo));
+    TRY(upload(c, &c->rds_h, rds));
+    TRY(upload(c, &c->rds_sq_h, rds_sq));
+    TRY(upload(c, &c->rrc_h, rrc));
+    TRY(upload(c, &c->audio_pp, pa.table));
+    TRY(upload(c, &c->audio_cnt, pa.cnt));
+    TRY(upload(c, &c->rdsbb_pp, pr.table));
+    TRY(upload(c, &c->rdsbb_cnt, pr.cnt));
+    // ---- extended streams ----
+    c->fm_stride = round_up((size_t)HIST + in.block_if, 64);
+    c->rf_stride = round_up((size_t)HIST + in.n_rds, 64);
+    c->fm_par = c->fm_stride * nch;
+    c->rf_par = c->rf_stride * nch;
+    float* base = nullptr;
+    TRY(dalloc(c, &base, 2 * c->fm_par)); c->fm = base + HIST;
+    TRY(dalloc(c, &base, 2 * c->fm_par)); c->sdc = base + HIST;
+    TRY(dalloc(c, &base, 2 * c->fm_par)); c->rband = base + HIST;
+    TRY(dalloc(c, &base, 2 * c->fm_par)); c->rdc = base + HIST;
+    TRY(dalloc(c, &base, 2 * c->rf_par)); c->rfilt = base + HIST;
+    c->plain_stride = round_up((size_t)in.block_if, 64);
+    c->pll_stride = round_up((size_t)in.block_if + 1, 64);
+    c->clean_stride = round_up((size_t)in.n_rds, 64);
+    TRY(dalloc(c, &c->pilot, c->plain_stride * nch));
+    TRY(dalloc(c, &c->band, c->plain_stride * nch));
+    TRY(dalloc(c, &c->gpilot, c->plain_stride * nch));
+    TRY(dalloc(c, &c->carrier, c->pll_stride * nch));
+    TRY(dalloc(c, &c->ipll, c->pll_stride * nch));
+    TRY(dalloc(c, &c->rds_clean, c->clean_stride * nch));
+    TRY(dalloc(c, &c->tail, (size_t)2 * nch * 2 * (T - 1)));
+    TRY(dalloc(c, &c->prev, (size_t)2 * nch));
+    TRY(dalloc(c, &c->st_pll, (size_t)nch));
+    TRY(dalloc(c, &c->rds_pll, (size_t)nch));
+    TRY(dalloc(c, &c->dec, (size_t)nch * DEC_STATE));
+    TRY(init_state(c, nullptr));
+#undef TRY
+    *out = c;
+    return SDR_OK;
+}
+
+int sdr_ctx_destroy(sdr_ctx* c) {
+    if (!c) return SDR_OK;
+    (void)hipSetDevice(c->device);
+    for (void* p : c->allocs) (void)hipFree(p);
+    delete c;
+    return SDR_OK;
+}
+
+int sdr_ctx_reset(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    return init_state(c, S(stream));
+}
+
+int sdr_ctx_info(const sdr_ctx* c, sdr_info* info) {
+    if (!c || !info) return fail(SDR_E_INVALID, "null argument");
+    *info = c->info;
+    return SDR_OK;
+}
+
+int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) {
+    if (!c || !iq) return fail(SDR_E_INVALID, "null argument");
+    const sdr_info& in = c->info;
+    if (iq_stride < (size_t)2 * in.block_iq || (iq_stride & 1) || (reinterpret_cast<uintptr_t>(iq) & 1))
+        return fail(SDR_E_INVALID, "iq_stride %zu < 2*block_iq %d or misaligned", iq_stride, 2 * in.block_iq);
+    const int p = c->parity ^ 1;
+    const int hp = c->ntaps - 1;
+    uint8_t* tail_in = c->tail + (size_t)(p ^ 1) * c->nch * 2 * hp;
+    uint8_t* tail_out = c->tail + (size_t)p * c->nch * 2 * hp;
+    const float2* prev_in = c->prev + (size_t)(p ^ 1) * c->nch;
+    float2* prev_out = c->prev + (size_t)p * c->nch;
+    const int tile = FIR_TILE;
+    dim3 grid(cdiv(in.block_if, tile), c->nch);
+    const size_t lds = frontend_lds_bytes(c->ntaps, tile, in.rf_decim);
+    hipLaunchKernelGGL(k_frontend, grid, dim3(BLK), lds, S(stream), iq, iq_stride, tail_in, tail_out, prev_in,
+                       prev_out, c->rf_h, c->ntaps, in.rf_decim, in.block_iq, in.block_if, tile,
+                       c->fm + p * c->fm_par, c->fm + (p ^ 1) * c->fm_par, c->fm_stride);
+    LAUNCH_CHECK();
+    c->parity = p;
+    c->block++;
+    return SDR_OK;
+}
+
+int sdr_get_fm_demod(sdr_ctx* c, float* fm, size_t fm_stride, void* stream) {
+    if (!c || !fm) return fail(SDR_E_INVALID, "null argument");
+    if (c->block < 0) return fail(SDR_E_INVALID, "no block processed yet");
+    const sdr_info& in = c->info;
+    HIP_TRY(hipMemcpy2DAsync(fm, fm_stride * sizeof(float), c->fm_cur(), c->fm_stride * sizeof(float),
+                             in.block_if * sizeof(float), c->nch, hipMemcpyDeviceToDevice, S(stream)));
+    return SDR_OK;
+}
+
+int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
+    if (!c || !audio) return fail(SDR_E_INVALID, "null argument");
+    if (c->block < 0 || c->mono_done == c->block) return fail(SDR_E_INVALID, "mono: no new block");
+    const sdr_info& in = c->info;
+    const int tile = 512;
+    dim3 grid(cdiv(in.n_audio, tile), c->nch);
+    const size_t lds = resample_lds_bytes(c->audio_L, in.audio_upsample, in.audio_decim, tile, 1);
+    const float* fm = c->fm_cur();
+    hipLaunchKernelGGL(k_resample<1>, grid, dim3(BLK), lds, S(stream), fm, fm, c->fm_stride, c->fm_stride,
+                       nullptr, nullptr, (size_t)0, (size_t)0, c->audio_pp, c->audio_cnt, c->audio_L,
+                       in.audio_upsample, in.audio_decim, in.n_audio, tile, -HIST, (void*)audio, audio_stride);
+    LAUNCH_CHECK();
+    c->mono_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_stereo(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
+    if (!c || !lr) return fail(SDR_E_INVALID, "null argument");
+    if (c->block < 0 || c->stereo_done == c->block) return fail(SDR_E_INVALID, "stereo: no new block");
+    const sdr_info& in = c->info;
+    hipStream_t s = S(stream);
+    const int n = in.block_if, T = c->ntaps;
+    const float* fm = c->fm_cur();
+    // pilot BPF (stereo.cpp:74) + band BPF (:80) from one staged window of fm_demod
+    dim3 gf(cdiv(n, FIR_TILE), c->nch);
+    hipLaunchKernelGGL((k_fir<2, false>), gf, dim3(BLK), fir_lds_bytes(T, 2, FIR_TILE, 1), s, fm, c->fm_stride, fm,
+                       c->fm_stride, c->pilot_h, c->stereo_h, T, 1, n, FIR_TILE, c->pilot, c->band, c->plain_stride);
+    LAUNCH_CHECK();
+    // PLL 19 kHz -> 38 kHz carrier (:77)
+    hipLaunchKernelGGL(k_pll, dim3(cdiv(c->nch, 64)), dim3(64), 0, s, c->pilot, c->plain_stride, n, c->nch, 19e3f,
+                       (float)(in.rf_Fs / in.rf_decim), c->carrier, c->pll_stride, c->st_pll, 2.0f, 0.0f, 0.01f);
+    LAUNCH_CHECK();
+    // mixer (:83-85) into the extended stereo_dc stream
+    const int p = c->parity;
+    float* sdc = c->sdc + p * c->fm_par;
+    hipLaunchKernelGGL(k_mix<false>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, c->band, c->plain_stride,
+                       c->carrier, c->pll_stride, n, sdc, c->sdc + (p ^ 1) * c->fm_par, c->fm_stride, 0);
+    LAUNCH_CHECK();
+    // mono delay (:88, exact 50-sample shift of fm_demod) + both resamplers + L/R (:94-107)
+    const int tile = 512;
+    dim3 gr(cdiv(in.n_audio, tile), c->nch);
+    const size_t lds = resample_lds_bytes(c->audio_L, in.audio_upsample, in.audio_decim, tile, 2);
+    hipLaunchKernelGGL(k_resample<2>, gr, dim3(BLK), lds, s, fm - 50, fm - 50, c->fm_stride, c->fm_stride, sdc, sdc,
+                       c->fm_stride, c->fm_stride, c->audio_pp, c->audio_cnt, c->audio_L, in.audio_upsample,
+                       in.audio_decim, in.n_audio, tile, -(HIST - 50), (void*)lr, lr_stride);
+    LAUNCH_CHECK();
+    c->stereo_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_rds_dsp(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->block < 0 || c->rds_dsp_done == c->block) return fail(SDR_E_INVALID, "rds: no new block");
+    const sdr_info& in = c->info;
+    hipStream_t s = S(stream);
+    const int n = in.block_if, T = c->ntaps, p = c->parity;
+    const float* fm = c->fm_cur();
+    float* rband = c->rband + p * c->fm_par;
+    float* rdc = c->rdc + p * c->fm_par;
+    float* rfilt = c->rfilt + p * c->rf_par;
+    dim3 gf(cdiv(n, FIR_TILE), c->nch);
+    // RDS band BPF (rds.cpp:105) into the extended rds_band stream
+    hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rband, c->rband + (p ^ 1) * c->fm_par,
+                       c->fm_stride, n);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL((k_fir<1, false>), gf, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, fm, c->fm_stride, fm,
+                       c->fm_stride, c->rds_h, nullptr, T, 1, n, FIR_TILE, rband, nullptr, c->fm_stride);
+    LAUNCH_CHECK();
+    // squaring (:111-113) + 114 kHz BPF (:116)
+    hipLaunchKernelGGL((k_fir<1, true>), gf, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, rband, c->fm_stride,
+                       rband, c->fm_stride, c->rds_sq_h, nullptr, T, 1, n, FIR_TILE, c->gpilot, nullptr,
+                       c->plain_stride);
+    LAUNCH_CHECK();
+    // PLL 114 kHz -> 57 kHz (:119)
+    hipLaunchKernelGGL(k_pll, dim3(cdiv(c->nch, 64)), dim3(64), 0, s, c->gpilot, c->plain_stride, n, c->nch, 114e3f,
+                       (float)in.if_Fs, c->ipll, c->pll_stride, c->rds_pll, 0.5f, 0.0f, 0.001f);
+    LAUNCH_CHECK();
+    // delay (:122) + mixer (:125-127) into the extended rds_dc stream
+    hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride, c->ipll,
+                       c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
+    LAUNCH_CHECK();
+    // 247/640 resampler (:130) into the extended rds_filt stream
+    hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rfilt, c->rfilt + (p ^ 1) * c->rf_par,
+                       c->rf_stride, in.n_rds);
+    LAUNCH_CHECK();
+    const int rtile = 256;
+    dim3 gr(cdiv(in.n_rds, rtile), c->nch);
+    hipLaunchKernelGGL(k_resample<0>, gr, dim3(BLK), resample_lds_bytes(c->rdsbb_L, 247, 640, rtile, 1), s, rdc, rdc,
+                       c->fm_stride, c->fm_stride, nullptr, nullptr, (size_t)0, (size_t)0, c->rdsbb_pp,
+                       c->rdsbb_cnt, c->rdsbb_L, 247, 640, in.n_rds, rtile, -HIST, (void*)rfilt, c->rf_stride);
+    LAUNCH_CHECK();
+    // RRC (:133)
+    dim3 gc(cdiv(in.n_rds, FIR_TILE), c->nch);
+    float* dst = rds_clean ? rds_clean : c->rds_clean;
+    const size_t dst_stride = rds_clean ? rds_stride : c->clean_stride;
+    hipLaunchKernelGGL((k_fir<1, false>), gc, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, rfilt, c->rf_stride,
+                       rfilt, c->rf_stride, c->rrc_h, nullptr, T, 1, in.n_rds, FIR_TILE, dst, nullptr, dst_stride);
+    LAUNCH_CHECK();
+    if (rds_clean) {
+        HIP_TRY(hipMemcpy2DAsync(c->rds_clean, c->clean_stride * sizeof(float), rds_clean, rds_stride * sizeof(float),
+                                 in.n_rds * sizeof(float), c->nch, hipMemcpyDeviceToDevice, s));
+    }
+    c->rds_dsp_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, size_t sym_stride, int32_t* nbits,
+                 uint8_t* bits, size_t bits_stride, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->rds_dsp_done != c->block || c->rds_bits_done == c->block)
+        return fail(SDR_E_INVALID, "rds_bits: run sdr_rds_dsp on a new block first");
+    const sdr_info& in = c->info;
+    hipLaunchKernelGGL(k_rds_bits, dim3(c->nch), dim3(64), 64 * sizeof(int), S(stream), c->rds_clean,
+                       c->clean_stride, in.n_rds, in.symbol_Fs, c->rds_on, c->dec, offset, nsym, symbols,
+                       sym_stride, nbits, bits, bits_stride);
+    LAUNCH_CHECK();
+    c->rds_bits_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_ctx_buffer(sdr_ctx* c, const char* name, const float** ptr, size_t* stride, int* len) {
+    if (!c || !name || !ptr || !stride || !len) return fail(SDR_E_INVALID, "null argument");
+    const sdr_info& in = c->info;
+    const int p = c->parity;
+    struct E { const char* n; const float* p; size_t s; int l; } tab[] = {
+        {"fm", c->fm_cur(), c->fm_stride, in.block_if},
+        {"pilot", c->pilot, c->plain_stride, in.block_if},
+        {"carrier", c->carrier, c->pll_stride, in.block_if + 1},
+        {"band", c->band, c->plain_stride, in.block_if},
+        {"stereo_dc", c->sdc + p * c->fm_par, c->fm_stride, in.block_if},
+        {"rds_band", c->rband + p * c->fm_par, c->fm_stride, in.block_if},
+        {"gen_pilot", c->gpilot, c->plain_stride, in.block_if},
+        {"ipll", c->ipll, c->pll_stride, in.block_if + 1},
+        {"rds_dc", c->rdc + p * c->fm_par, c->fm_stride, in.block_if},
+        {"rds_filt", c->rfilt + p * c->rf_par, c->rf_stride, in.n_rds},
+        {"rds_clean", c->rds_clean, c->clean_stride, in.n_rds},
+    };
+    for (const E& e : tab) {
+        if (std::strcmp(e.n, name) == 0) {
+            *ptr = e.p;
+            *stride = e.s;
+            *len = e.l;
+            return SDR_OK;
+        }
+    }
+    return fail(SDR_E_INVALID, "unknown buffer %s", name);
+}
+
+// ------------------------------------------------------------------ batched primitives
+int sdr_convolve_fir(float* y, size_t y_stride, const float* x, size_t x_stride, int nch, int nx, const float* h,
+                     int ntaps, float* state, int nstate, int D, void* stream) {
+    if (!y || !x || !h || !state || nch <= 0 || nx <= 0 || ntaps <= 0 || D <= 0 || nstate < ntaps - 1)
+        return fail(SDR_E_INVALID, "convolve_fir: bad arguments (nstate must be >= ntaps-1)");
+    const int ny = nx / D;
+    if (ny > 0) {
+        const int tile = FIR_TILE;
+        const size_t lds = fir_lds_bytes(ntaps, 1, tile, D);
+        if (lds > 160 * 1024) return fail(SDR_E_INVALID, "convolve_fir: ntaps*D too large for one tile");
+        hipLaunchKernelGGL((k_fir<1, false>), dim3(cdiv(ny, tile), nch), dim3(BLK), lds, S(stream), x, x_stride,
+                           state + nstate, (size_t)nstate, h, nullptr, ntaps, D, ny, tile, y, nullptr, y_stride);
+        LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_state_update, dim3(nch), dim3(256), 0, S(stream), state, nstate, x, x_stride, nx);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+namespace {
+struct PPCache {
+    std::mutex m;
+    const float* h = nullptr;
+    int ntaps = 0, U = 0;
+    std::vector<float> host;
+    float* table = nullptr;
+    int* cnt = nullptr;
+    int L = 0;
+};
+PPCache g_pp;
+}  // namespace
+
+int sdr_convolve_fir_resample(float* y, size_t y_stride, const float* x, size_t x_stride, int nch, int nx,
+                              const float* h, int ntaps, float* state, int nstate, int U, int D, void* stream) {
+    if (!y || !x || !h || !state || nch <= 0 || nx <= 0 || ntaps <= 0 || U <= 0 || D <= 0)
+        return fail(SDR_E_INVALID, "convolve_fir_resample: bad arguments");
+    const int ny = (int)(((long long)nx * U) / D);
+    // polyphase table of the (device) taps, cached per (h, ntaps, U)
+    std::lock_guard<std::mutex> lk(g_pp.m);
+    std::vector<float> hh(ntaps);
+    HIP_TRY(hipMemcpy(hh.data(), h, ntaps * sizeof(float), hipMemcpyDeviceToHost));
+    if (g_pp.h != h || g_pp.ntaps != ntaps || g_pp.U != U || g_pp.host != hh) {
+        if (g_pp.table) (void)hipFree(g_pp.table);
+        if (g_pp.cnt) (void)hipFree(g_pp.cnt);
+        Polyphase pp = make_polyphase(hh, U);
+        HIP_TRY(hipMalloc(&g_pp.table, pp.table.size() * sizeof(float)));
+        HIP_TRY(hipMalloc(&g_pp.cnt, pp.cnt.size() * sizeof(int)));
+        HIP_TRY(hipMemcpy(g_pp.table, pp.table.data(), pp.table.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(g_pp.cnt, pp.cnt.data(), pp.cnt.size() * sizeof(int), hipMemcpyHostToDevice));
+        g_pp.h = h; g_pp.ntaps = ntaps; g_pp.U = U; g_pp.host = hh; g_pp.L = pp.L;
+    }
+    // the deepest look-back is output 0: x[-(ceil(ntaps/U)-1)] (100 in every mode)
+    const int lookback = (ntaps + U - 1) / U - 1;
+    if (nstate < lookback)
+        return fail(SDR_E_INVALID, "convolve_fir_resample: nstate %d < look-back %d", nstate, lookback);
+    if (ny > 0) {
+        const int tile = 256;
+        const size_t lds = resample_lds_bytes(g_pp.L, U, D, tile, 1);
+        hipLaunchKernelGGL(k_resample<0>, dim3(cdiv(ny, tile), nch), dim3(BLK), lds, S(stream), x, state + nstate,
+                           x_stride, (size_t)nstate, nullptr, nullptr, (size_t)0, (size_t)0, g_pp.table, g_pp.cnt,
+                           g_pp.L, U, D, ny, tile, -nstate, (void*)y, y_stride);
+        LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_state_update, dim3(nch), dim3(256), 0, S(stream), state, nstate, x, x_stride, nx);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+int sdr_fm_demod(float* out, size_t out_stride, const float* I, const float* Q, size_t iq_stride, int nch, int n,
+                 float* prev, void* stream) {
+    if (!out || !I || !Q || !prev || nch <= 0 || n <= 0) return fail(SDR_E_INVALID, "fm_demod: bad arguments");
+    hipLaunchKernelGGL(k_demod, dim3(cdiv(n, BLK), nch), dim3(BLK), 0, S(stream), out, out_stride, I, Q, iq_stride, n,
+                       reinterpret_cast<const float2*>(prev));
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_demod_prev, dim3(cdiv(nch, 64)), dim3(64), 0, S(stream), reinterpret_cast<float2*>(prev), I,
+                       Q, iq_stride, n, nch);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, int nch, int n, float freq, float Fs,
+              sdr_pll_state* state, float ncoScale, float phaseAdjust, float normBandwidth, void* stream) {
+    if (!out || !in || !state || nch <= 0 || n < 0) return fail(SDR_E_INVALID, "fmpll: bad arguments");
+    hipLaunchKernelGGL(k_pll, dim3(cdiv(nch, 64)), dim3(64), 0, S(stream), in, in_stride, n, nch, freq, Fs, out,
+                       out_stride, state, ncoScale, phaseAdjust, normBandwidth);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+int sdr_cdr(int32_t* offset, const float* x, size_t x_stride, int nch, int n, int sps, void* stream) {
+    if (!offset || !x || nch <= 0 || n < 0 || sps <= 0 || sps > 64) return fail(SDR_E_INVALID, "cdr: bad arguments");
+    hipLaunchKernelGGL(k_cdr, dim3(nch), dim3(64), 64 * sizeof(int), S(stream), offset, x, x_stride, n, sps);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+"""CPU: the C-ABI library loads, exports every symbol include/sdr_amd.h declares, rejects bad
+arguments without touching a GPU, and its host-side tap design equals the reference's taps."""
+from __future__ import annotations
+
+import ctypes as C
+import re
+
+import numpy as np
+
+from conftest import ROOT
+
+
+def _declared(header: str) -> list[str]:
+    text = (ROOT / "include" / header).read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sdr_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib = pkg.lib()
+    names = _declared("sdr_amd.h")
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_errors_are_status_codes(pkg):
+    lib = pkg.lib()
+    assert lib.sdr_version() >= 1
+    assert lib.sdr_ctx_info(None, None) == -1
+    assert b"null" in lib.sdr_last_error()
+    assert lib.sdr_frontend(None, None, 0, None) == -1
+    assert lib.sdr_convolve_fir(None, 0, None, 0, 1, 10, None, 101, None, 100, 1, None) == -1
+    assert lib.sdr_impulse_response_lpf(2.4e6, 1e5, 101, None) == -1
+
+
+def test_product_taps_equal_reference_taps(pkg, golden):
+    cases = {
+        "rf": pkg.impulse_response_lpf(2.4e6, 1e5, 101),
+        "audio": pkg.impulse_response_lpf(240000.0, 16000.0, 101, 1),
+        "pilot": pkg.impulse_response_bpf(240000.0, 18.5e3, 19.5e3, 101),
+        "stereo": pkg.impulse_response_bpf(240000.0, 22e3, 54e3, 101),
+        "carrier": pkg.impulse_response_bpf(240000.0, 37.5e3, 38.5e3, 101),
+        "apf": pkg.impulse_response_apf(1.0, 101),
+        "rds": pkg.impulse_response_bpf(240000.0, 54e3, 60e3, 101),
+        "rds_sq": pkg.impulse_response_bpf(240000.0, 113.5e3, 114.5e3, 101),
+        "rds_bb": pkg.impulse_response_lpf(240000.0 * 247, 3e3, 24947, 247),
+        "rrc": pkg.impulse_response_rrc(2375.0 * 39, 101),
+    }
+    for name, h in cases.items():
+        assert np.array_equal(h.view(np.uint32), golden["taps_" + name].view(np.uint32)), name
+
+
+def test_struct_layouts(pkg):
+    # pllblock_args: 4 floats, a double, a float -> 32 bytes with the double 8-aligned (include/pll.h:10-17)
+    assert C.sizeof(pkg.PllState) == 32
+    assert pkg.PllState.trigOffset.offset == 16
+    assert C.sizeof(pkg.Info) == 15 * 4

@@ -1,0 +1,7 @@
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 300 python -m pytest ${PYTEST_ARGS:-tests -x -q -m gpu} > gpurun_out/pytest_gpu1.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+tail -30 gpurun_out/pytest_gpu1.log
+exit $rc
