@@ -35,6 +35,7 @@ extern "C" {
 
 /* Context flags */
 #define SDR_FLAG_FAST_FRONTEND 0x1  /* FMA front end: fm_demod within 1e-6 rel., not bit-exact */
+#define SDR_FLAG_PLL_LIBM 0x2       /* PLL via per-step f64 libm calls (A/B reference; env SDR_PLL=libm) */
 
 /* pllblock_args, include/pll.h:10-17 (same field order and types) */
 typedef struct sdr_pll_state {

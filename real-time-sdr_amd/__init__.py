@@ -27,6 +27,7 @@ SDR_OK = 0
 SDR_MAX_SYMS = 256
 SDR_MAX_BITS = 256
 FLAG_FAST_FRONTEND = 0x1
+FLAG_PLL_LIBM = 0x2
 
 _lib = None
 

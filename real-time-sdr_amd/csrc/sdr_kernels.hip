@@ -26,11 +26,13 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdarg>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "sdr_amd.h"
+#include "pll_math.h"
 
 #pragma clang fp contract(off)
 
@@ -261,12 +263,163 @@ __global__ __launch_bounds__(BLK) void k_resample(const float* __restrict__ xa, 
 }
 
 // ------------------------------------------------------------------------------------------
-// PLL / NCO, pll.cpp:4-61: one lane per channel, the recurrence is serial in time.
+// PLL / NCO, pll.cpp:4-61. One lane per channel: the recurrence is serial in time.
+//
+// k_pll_libm: the literal restatement (f64 OCML atan2/sincos per step), kept as the A/B
+// reference (flag SDR_FLAG_PLL_LIBM) and used for chunk redo.
+// k_pll: the same recurrence with pll_math.h's correctly-rounded fast paths. Each 64-step chunk
+// runs branch-free; if any step of a lane reported an ambiguous f32 rounding (~6.6e-6 per step)
+// the lane restores its chunk snapshot and redoes the chunk with per-step f64-libm fallbacks.
+// Both write out[0] = lastCarrier and out[i+1] = t_i (the f32 NCO phase); k_nco_out then turns
+// t_i into cos(t_i*ncoScale + phaseAdjust) in parallel (pll.cpp:52) and updates lastCarrier.
 // ------------------------------------------------------------------------------------------
+struct PllRegs {
+    float fbI, fbQ, integ, ph;
+    double toff, c, s, phi;
+};
+
+__device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
+    PllRegs r;
+    r.fbI = st.feedbackI;
+    r.fbQ = st.feedbackQ;
+    r.integ = st.integrator;
+    r.ph = st.phaseEst;
+    r.toff = st.trigOffset;
+    // rotation reference for the phase detector: the previous step's trigArg (pll.cpp:47)
+    const float t_prev = (float)(w * r.toff + (double)r.ph);
+    const pllm::SinCos sc = pllm::sincos_f32(t_prev);
+    r.c = sc.c;
+    r.s = sc.s;
+    r.phi = (__builtin_fabs((double)t_prev) < pllm::T_MAX) ? sc.phi : __builtin_nan("");
+    return r;
+}
+
+// Per-chunk accumulators of the fast path's proof obligations (kept in VGPRs: no SGPR masks).
+struct PllProof {
+    double dsum = 0.0;      // sum |residual angle|        needs < 2^-18 (a sum, so NaN/inf propagate:
+                            // X == 0 gives d = NaN, and a NaN e, t or phase can only come from a NaN d)
+    double emax = 0.0;      // max |e|                     needs < pi - 2^-30
+    double tmax = 0.0;      // max |t|                     needs < 2^30 (reduction range)
+    uint32_t split = 0u;    // OR of phase-detector rounding splits, needs 0
+    uint32_t tie = ~0u;     // min of sin/cos tie distances, needs > 128
+    __device__ __forceinline__ bool ok() const {
+        return (dsum < 0x1p-18) & (emax < pllm::PI - 0x1p-30) & (tmax < pllm::T_MAX) & (split == 0u) & (tie > 128u);
+    }
+};
+
+// one step; CHECKED: fall back to the f64 libm path whenever the fast path cannot prove the f32
+// rounding (used for chunk redo and short tails).
+template <bool CHECKED>
+__device__ __forceinline__ void pll_step(PllRegs& r, float x, float Kp, float Ki, double w, float& t_out,
+                                         PllProof& pf) {
+    const float eI = x * r.fbI;                               // pll.cpp:36
+    const float eQ = x * (-r.fbQ);                            // pll.cpp:37
+    const pllm::Phase p = pllm::phase_detect(eI, eQ, r.c, r.s, r.phi);
+    float e = (float)p.e;
+    if (CHECKED && !p.ok) e = (float)atan2((double)eQ, (double)eI);  // pll.cpp:39
+    r.integ = r.integ + Ki * e;                               // pll.cpp:41
+    r.ph = r.ph + Kp * e + r.integ;                           // pll.cpp:42
+    r.toff += 1.0;                                            // pll.cpp:46
+    const float t = (float)(w * r.toff + (double)r.ph);       // pll.cpp:47
+    const pllm::SinCos sc = pllm::sincos_f32(t);
+    r.c = sc.c;
+    r.s = sc.s;
+    r.phi = sc.phi;
+    r.fbI = (float)sc.c;                                      // pll.cpp:49
+    r.fbQ = (float)sc.s;                                      // pll.cpp:50
+    if (CHECKED && !sc.ok) {
+        double sv, cv;
+        sincos((double)t, &sv, &cv);
+        r.fbI = (float)cv;
+        r.fbQ = (float)sv;
+        r.c = cv;
+        r.s = sv;
+        if (!(__builtin_fabs((double)t) < pllm::T_MAX)) r.phi = __builtin_nan("");
+    }
+    if (!CHECKED) {
+        pf.dsum = pf.dsum + __builtin_fabs(p.d);
+        pf.emax = fmax(pf.emax, __builtin_fabs(p.e));      // NaN-ignoring max is fine: see dsum
+        pf.tmax = fmax(pf.tmax, __builtin_fabs((double)t));
+        pf.split |= p.split;
+        pf.tie = min(pf.tie, sc.tie);
+    }
+    t_out = t;
+}
+
+constexpr int PLL_CHUNK = 16;
+
+// VEC: x rows and the t buffer are 16-byte aligned with strides that are multiples of 4, so a
+// chunk's inputs are prefetched with float4 loads one chunk ahead and the 16 phases are stored
+// with float4 stores -- the unrolled chunk itself touches no memory.
+template <bool VEC>
 __global__ __launch_bounds__(64) void k_pll(const float* __restrict__ in, size_t in_stride, int n, int nch,
-                                            float freq, float Fs, float* __restrict__ out, size_t out_stride,
-                                            sdr_pll_state* __restrict__ st, float ncoScale, float phaseAdjust,
-                                            float normBandwidth) {
+                                            float freq, float Fs, float* __restrict__ tbuf, size_t t_stride,
+                                            float* __restrict__ out, size_t out_stride,
+                                            sdr_pll_state* __restrict__ st, float normBandwidth) {
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= nch) return;
+    const float Cp = 2.666;
+    const float Ci = 3.555;
+    const float Kp = normBandwidth * Cp;
+    const float Ki = normBandwidth * normBandwidth * Ci;
+    const double w = 2 * 3.14159265358979323846 * (freq / Fs);
+    const sdr_pll_state s0 = st[ch];
+    const float* x = in + (size_t)ch * in_stride;
+    float* tb = tbuf + (size_t)ch * t_stride;
+    out[(size_t)ch * out_stride] = s0.lastCarrier;             // pll.cpp:18
+    PllRegs r = pll_load(s0, w);
+    const int nfull = VEC ? (n / PLL_CHUNK) * PLL_CHUNK : 0;
+    float4 xa[PLL_CHUNK / 4];
+    if (nfull > 0) {
+#pragma unroll
+        for (int k = 0; k < PLL_CHUNK / 4; k++) xa[k] = reinterpret_cast<const float4*>(x)[k];
+    }
+    for (int i0 = 0; i0 < nfull; i0 += PLL_CHUNK) {
+        float4 xn[PLL_CHUNK / 4];
+        const bool more = i0 + PLL_CHUNK < nfull;
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < PLL_CHUNK / 4; k++) xn[k] = reinterpret_cast<const float4*>(x + i0 + PLL_CHUNK)[k];
+        }
+        const PllRegs snap = r;
+        PllProof pf;
+        float tv[PLL_CHUNK];
+#pragma unroll
+        for (int j = 0; j < PLL_CHUNK; j++) {
+            const float4 v4 = xa[j >> 2];
+            const float xv = (j & 3) == 0 ? v4.x : (j & 3) == 1 ? v4.y : (j & 3) == 2 ? v4.z : v4.w;
+            pll_step<false>(r, xv, Kp, Ki, w, tv[j], pf);
+        }
+        if (!pf.ok()) {
+            r = snap;
+            for (int j = 0; j < PLL_CHUNK; j++) pll_step<true>(r, x[i0 + j], Kp, Ki, w, tb[i0 + j], pf);
+        } else {
+#pragma unroll
+            for (int k = 0; k < PLL_CHUNK / 4; k++)
+                reinterpret_cast<float4*>(tb + i0)[k] = make_float4(tv[4 * k], tv[4 * k + 1], tv[4 * k + 2], tv[4 * k + 3]);
+        }
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < PLL_CHUNK / 4; k++) xa[k] = xn[k];
+        }
+    }
+    {
+        PllProof pf;
+        for (int i = nfull; i < n; i++) pll_step<true>(r, x[i], Kp, Ki, w, tb[i], pf);
+    }
+    sdr_pll_state s1 = s0;
+    s1.feedbackI = r.fbI;
+    s1.feedbackQ = r.fbQ;
+    s1.integrator = r.integ;
+    s1.phaseEst = r.ph;
+    s1.trigOffset = r.toff;
+    st[ch] = s1;                                               // lastCarrier: k_nco_out
+}
+
+__global__ __launch_bounds__(64) void k_pll_libm(const float* __restrict__ in, size_t in_stride, int n, int nch,
+                                                 float freq, float Fs, float* __restrict__ tbuf, size_t t_stride,
+                                                 float* __restrict__ out, size_t out_stride,
+                                                 sdr_pll_state* __restrict__ st, float normBandwidth) {
     const int ch = blockIdx.x * blockDim.x + threadIdx.x;
     if (ch >= nch) return;
     const float Cp = 2.666;
@@ -276,11 +429,10 @@ __global__ __launch_bounds__(64) void k_pll(const float* __restrict__ in, size_t
     const double w = 2 * 3.14159265358979323846 * (freq / Fs);  // 2*PI*(freq/Fs), pll.cpp:47
     sdr_pll_state s = st[ch];
     const float* x = in + (size_t)ch * in_stride;
-    float* o = out + (size_t)ch * out_stride;
-    o[0] = s.lastCarrier;
+    out[(size_t)ch * out_stride] = s.lastCarrier;
+    float* o = tbuf + (size_t)ch * t_stride;
     float fbI = s.feedbackI, fbQ = s.feedbackQ, integ = s.integrator, ph = s.phaseEst;
     double toff = s.trigOffset;
-    float last = s.lastCarrier;
     for (int i = 0; i < n; i++) {
         const float xi = x[i];
         const float eI = xi * fbI;
@@ -294,16 +446,32 @@ __global__ __launch_bounds__(64) void k_pll(const float* __restrict__ in, size_t
         sincos((double)t, &sv, &cv);
         fbI = (float)cv;
         fbQ = (float)sv;
-        last = (float)cos((double)(t * ncoScale + phaseAdjust));
-        o[i + 1] = last;
+        o[i] = t;
     }
     s.feedbackI = fbI;
     s.feedbackQ = fbQ;
     s.integrator = integ;
     s.phaseEst = ph;
     s.trigOffset = toff;
-    s.lastCarrier = last;
     st[ch] = s;
+}
+
+// out[ch][i+1]: t_i -> (float)cos((double)(t_i*ncoScale + phaseAdjust)) (pll.cpp:52), in parallel;
+// lastCarrier <- out[ch][n] (pll.cpp:58)
+__global__ __launch_bounds__(BLK) void k_nco_out(const float* __restrict__ tbuf, size_t t_stride,
+                                                 float* __restrict__ out, size_t out_stride, int n,
+                                                 sdr_pll_state* __restrict__ st, float ncoScale, float phaseAdjust) {
+    const int ch = blockIdx.y;
+    const int i = blockIdx.x * BLK + threadIdx.x;
+    if (i >= n) return;
+    float* o = out + (size_t)ch * out_stride + 1;
+    const float t = tbuf[(size_t)ch * t_stride + i];
+    const float a = t * ncoScale + phaseAdjust;
+    const pllm::SinCos sc = pllm::sincos_f32(a);
+    float v = (float)sc.c;
+    if (!sc.ok) v = (float)cos((double)a);
+    o[i] = v;
+    if (i == n - 1) st[ch].lastCarrier = v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -546,6 +714,41 @@ Polyphase make_polyphase(const std::vector<float>& h, int U) {
     return p;
 }
 
+// PLL + NCO output: k_pll (fast, default) or k_pll_libm (SDR_FLAG_PLL_LIBM / env SDR_PLL=libm)
+bool pll_libm_env() {
+    static const bool v = [] {
+        const char* e = std::getenv("SDR_PLL");
+        return e && std::strcmp(e, "libm") == 0;
+    }();
+    return v;
+}
+
+int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
+               size_t t_stride, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale, float phaseAdjust,
+               float bw, hipStream_t s) {
+    const dim3 g(cdiv(nch, 64)), b(64);
+    const bool vec = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (in_stride % 4 == 0) &&
+                     (reinterpret_cast<uintptr_t>(tbuf) % 16 == 0) && (t_stride % 4 == 0);
+    if (libm || pll_libm_env()) {
+        hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, in, in_stride, n, nch, freq, Fs, tbuf, t_stride, out, out_stride,
+                           st, bw);
+    } else if (vec) {
+        hipLaunchKernelGGL(k_pll<true>, g, b, 0, s, in, in_stride, n, nch, freq, Fs, tbuf, t_stride, out, out_stride,
+                           st, bw);
+    } else {
+        hipLaunchKernelGGL(k_pll<false>, g, b, 0, s, in, in_stride, n, nch, freq, Fs, tbuf, t_stride, out,
+                           out_stride, st, bw);
+    }
+    LAUNCH_CHECK();
+    if (n > 0) {
+        hipLaunchKernelGGL(k_nco_out, dim3(cdiv(n, BLK), nch), dim3(BLK), 0, s, tbuf, t_stride, out, out_stride, n, st,
+                           ncoScale, phaseAdjust);
+        LAUNCH_CHECK();
+    }
+    return SDR_OK;
+}
+
+
 }  // namespace
 
 // ============================================================================================
@@ -567,7 +770,7 @@ struct sdr_ctx {
     size_t fm_par = 0, rf_par = 0;                      // parity offsets in elements
     // plain per-block buffers
     float *pilot = nullptr, *band = nullptr, *gpilot = nullptr, *carrier = nullptr, *ipll = nullptr,
-          *rds_clean = nullptr;
+          *rds_clean = nullptr, *t_st = nullptr, *t_rds = nullptr;
     size_t plain_stride = 0, pll_stride = 0, clean_stride = 0;
     // state
     uint8_t* tail = nullptr;                            // [2][nch][2*(ntaps-1)]
@@ -726,6 +929,8 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     TRY(dalloc(c, &c->pilot, c->plain_stride * nch));
     TRY(dalloc(c, &c->band, c->plain_stride * nch));
     TRY(dalloc(c, &c->gpilot, c->plain_stride * nch));
+    TRY(dalloc(c, &c->t_st, c->plain_stride * nch));
+    TRY(dalloc(c, &c->t_rds, c->plain_stride * nch));
     TRY(dalloc(c, &c->carrier, c->pll_stride * nch));
     TRY(dalloc(c, &c->ipll, c->pll_stride * nch));
     TRY(dalloc(c, &c->rds_clean, c->clean_stride * nch));
@@ -821,9 +1026,12 @@ int sdr_stereo(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
                        c->fm_stride, c->pilot_h, c->stereo_h, T, 1, n, FIR_TILE, c->pilot, c->band, c->plain_stride);
     LAUNCH_CHECK();
     // PLL 19 kHz -> 38 kHz carrier (:77)
-    hipLaunchKernelGGL(k_pll, dim3(cdiv(c->nch, 64)), dim3(64), 0, s, c->pilot, c->plain_stride, n, c->nch, 19e3f,
-                       (float)(in.rf_Fs / in.rf_decim), c->carrier, c->pll_stride, c->st_pll, 2.0f, 0.0f, 0.01f);
-    LAUNCH_CHECK();
+    {
+        const int r = launch_pll(c->flags & SDR_FLAG_PLL_LIBM, c->pilot, c->plain_stride, n, c->nch, 19e3f,
+                                 (float)(in.rf_Fs / in.rf_decim), c->t_st, c->plain_stride, c->carrier, c->pll_stride,
+                                 c->st_pll, 2.0f, 0.0f, 0.01f, s);
+        if (r) return r;
+    }
     // mixer (:83-85) into the extended stereo_dc stream
     const int p = c->parity;
     float* sdc = c->sdc + p * c->fm_par;
@@ -866,9 +1074,12 @@ int sdr_rds_dsp(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
                        c->plain_stride);
     LAUNCH_CHECK();
     // PLL 114 kHz -> 57 kHz (:119)
-    hipLaunchKernelGGL(k_pll, dim3(cdiv(c->nch, 64)), dim3(64), 0, s, c->gpilot, c->plain_stride, n, c->nch, 114e3f,
-                       (float)in.if_Fs, c->ipll, c->pll_stride, c->rds_pll, 0.5f, 0.0f, 0.001f);
-    LAUNCH_CHECK();
+    {
+        const int r = launch_pll(c->flags & SDR_FLAG_PLL_LIBM, c->gpilot, c->plain_stride, n, c->nch, 114e3f,
+                                 (float)in.if_Fs, c->t_rds, c->plain_stride, c->ipll, c->pll_stride, c->rds_pll, 0.5f,
+                                 0.0f, 0.001f, s);
+        if (r) return r;
+    }
     // delay (:122) + mixer (:125-127) into the extended rds_dc stream
     hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride, c->ipll,
                        c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
@@ -1023,10 +1234,13 @@ int sdr_fm_demod(float* out, size_t out_stride, const float* I, const float* Q, 
 int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, int nch, int n, float freq, float Fs,
               sdr_pll_state* state, float ncoScale, float phaseAdjust, float normBandwidth, void* stream) {
     if (!out || !in || !state || nch <= 0 || n < 0) return fail(SDR_E_INVALID, "fmpll: bad arguments");
-    hipLaunchKernelGGL(k_pll, dim3(cdiv(nch, 64)), dim3(64), 0, S(stream), in, in_stride, n, nch, freq, Fs, out,
-                       out_stride, state, ncoScale, phaseAdjust, normBandwidth);
-    LAUNCH_CHECK();
-    return SDR_OK;
+    const size_t ts = round_up((size_t)std::max(n, 1), 4);
+    float* tbuf = nullptr;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tbuf), ts * nch * sizeof(float), S(stream)));
+    const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, tbuf, ts, out, out_stride, state, ncoScale,
+                             phaseAdjust, normBandwidth, S(stream));
+    HIP_TRY(hipFreeAsync(tbuf, S(stream)));
+    return r;
 }
 
 int sdr_cdr(int32_t* offset, const float* x, size_t x_stride, int nch, int n, int sps, void* stream) {

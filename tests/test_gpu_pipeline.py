@@ -142,3 +142,25 @@ def test_reset_restarts_stream(pkg, synth, torch_cuda):
     with pytest.raises(pkg.SdrError):
         pipe.stereo()   # at most once per block
     pipe.close()
+
+
+def test_fast_pll_matches_libm_pll(pkg, synth, torch_cuda):
+    """A/B on the GPU: the correctly-rounded fast PLL (default) against the per-step f64-libm PLL
+    (SDR_FLAG_PLL_LIBM, the literal pll.cpp restatement) -- identical NCO outputs and RDS bits."""
+    torch = torch_cuda
+    nch, nb = 48, 40
+    iqs = [channel_input(synth, 200 + c, nb) for c in range(nch)]
+    d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
+    pa = pkg.Pipeline(nch)
+    pb = pkg.Pipeline(nch, flags=pkg.FLAG_PLL_LIBM)
+    for b in range(nb):
+        for p in (pa, pb):
+            p.frontend(d[b])
+            p.stereo()
+            p.rds()
+        for name in ("carrier", "ipll"):
+            xa, xb = pa.buffer(name).cpu().numpy(), pb.buffer(name).cpu().numpy()
+            assert np.array_equal(xa.view(np.uint32), xb.view(np.uint32)), f"{name} block {b}"
+        assert torch.equal(pa.nbits, pb.nbits) and torch.equal(pa.bits, pb.bits)
+    pa.close()
+    pb.close()
