@@ -5,6 +5,7 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 PKG      := real-time-sdr_amd
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-flush-denormals-to-zero \
+            -mllvm -pragma-unroll-threshold=1000000 \
             -Wall -Iinclude
 LIB      := $(PKG)/libsdr_amd.so
 SRCS     := $(PKG)/csrc/sdr_kernels.hip $(PKG)/csrc/sdr_taps.cpp

@@ -152,6 +152,167 @@ __global__ __launch_bounds__(BLK) void k_frontend(
 }
 
 // ------------------------------------------------------------------------------------------
+// Front end v2 (register-blocked). Each thread computes R consecutive decimated outputs (I and Q
+// as one packed f32 pair) by streaming its input window in DESCENDING sample order: every output
+// then still accumulates its taps in ascending k (filter.cpp:110-116), while each input sample is
+// converted once and feeds up to R outputs. Conversion: u8 -> signed byte (u ^ 0x80 = u - 128)
+// -> f32 m via SDWA sext; with taps pre-scaled by 2^-7 (hs = h/128, exact) the product
+// fl(hs*m) equals the reference's fl(h*x), x = (u-128)/128, bit for bit.
+//   exact: v_pk_mul_f32 + v_pk_add_f32 (separate roundings, like filter.cpp:115)
+//   FAST:  v_pk_fma_f32 (one rounding per tap; fm_demod within ~1e-6 relative)
+// A tile computes TILE = 256*R outputs starting one before the first fm_demod sample it writes
+// (the discriminator's carry, demod.cpp:16), so tiles advance by TILE-1. The u8 window is staged
+// in LDS with coalesced dword loads (D even) or u16 loads (D odd).
+// ------------------------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// One input sample S (descending) of the register-blocked FIR: up to R independent packed MACs,
+// then recursion to S-1 -- complete unrolling with compile-time chunk and tap indices. A
+// sched_barrier closes every sample so the scheduler keeps the sample-major order (ILP across the
+// R accumulators, each product next to its add) instead of hoisting products or serialising one
+// output's chain; the LDS chunk two chunks ahead is read at each chunk boundary.
+constexpr int FE_PF = 3;   // tap rows prefetched this many samples ahead (rotating register ring)
+
+template <int R, int D, bool FAST>
+__global__ __launch_bounds__(64) void k_frontend2(
+    const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
+    uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
+    const float* __restrict__ hs, int block_iq, int block_if,
+    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride) {
+    constexpr int NT = 101, HP = NT - 1, NTH = 64;
+    constexpr int TILE = NTH * R;
+    constexpr int WIN = (TILE - 1) * D + NT;          // staged samples (u8 I/Q pairs)
+    constexpr int TWIN = (R - 1) * D + NT;            // samples one thread reads
+    constexpr int TCH = (2 * TWIN + 15) / 16;         // 16-byte LDS chunks per thread window
+    constexpr int LDS_BYTES = ((2 * WIN + 15) / 16) * 16 + 32;
+    __shared__ __attribute__((aligned(16))) uint8_t sw[LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) float stt[TWIN * R];
+    const int ch = blockIdx.y, t = threadIdx.x;
+    for (int i = t; i < TWIN * R / 4; i += NTH)
+        reinterpret_cast<float4*>(stt)[i] = reinterpret_cast<const float4*>(hs)[i];
+    const int c0 = blockIdx.x * (TILE - 1) - 1;       // first decimated output (the carry)
+    const int m0 = c0 * D - HP;                       // first staged sample
+    const uint8_t* src = iq + (size_t)ch * iq_stride;
+    const uint8_t* tin = tail_in + (size_t)ch * 2 * HP;
+    const bool interior = (m0 >= 0) && (m0 + WIN <= block_iq);
+    // ---- stage the window ----
+    if (D % 2 == 0) {
+        constexpr int NG = (2 * WIN + 3) / 4;         // dword granules (2 samples each)
+        uint32_t* sd = reinterpret_cast<uint32_t*>(sw);
+        if (interior) {
+            const uint32_t* g = reinterpret_cast<const uint32_t*>(src + 2 * m0);
+#pragma unroll 8
+            for (int i = t; i < NG; i += NTH) sd[i] = g[i];
+        } else {
+            for (int i = t; i < NG; i += NTH) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int m = m0 + 2 * i + h;
+                    uint32_t pr = 0x8080u;   // outside the stream: u8 128 == 0.0f (zero state)
+                    if (m >= 0 && m < block_iq) pr = reinterpret_cast<const uint16_t*>(src)[m];
+                    else if (m < 0 && m >= -HP) pr = reinterpret_cast<const uint16_t*>(tin)[HP + m];
+                    v |= pr << (16 * h);
+                }
+                sd[i] = v;
+            }
+        }
+    } else {
+        uint16_t* sh16 = reinterpret_cast<uint16_t*>(sw);
+        for (int i = t; i < WIN; i += NTH) {
+            const int m = m0 + i;
+            uint16_t pr = 0x8080u;
+            if (m >= 0 && m < block_iq) pr = reinterpret_cast<const uint16_t*>(src)[m];
+            else if (m < 0 && m >= -HP) pr = reinterpret_cast<const uint16_t*>(tin)[HP + m];
+            sh16[i] = pr;
+        }
+    }
+    __syncthreads();
+    // ---- FIR: R outputs per thread, samples in descending order ----
+    uint4 chunk[TCH];
+    const uint4* tw = reinterpret_cast<const uint4*>(sw + 2 * t * R * D);
+    chunk[TCH - 1] = tw[TCH - 1];
+    if (TCH >= 2) chunk[TCH - 2] = tw[TCH - 2];
+    f32x2 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
+    const float4* tt4 = reinterpret_cast<const float4*>(stt);
+    float4 ring[FE_PF][R / 4];
+#pragma unroll
+    for (int j = 0; j < FE_PF; j++) {
+        const int S0 = TWIN - 1 - j;
+#pragma unroll
+        for (int q = 0; q < R / 4; q++) ring[S0 % FE_PF][q] = tt4[S0 * (R / 4) + q];
+    }
+    // Samples in descending order, completely unrolled (the build raises clang's pragma-unroll
+    // threshold): chunk, tap-ring and accumulator indices are compile-time constants. A
+    // sched_barrier closes every sample so the scheduler keeps the sample-major order (ILP across
+    // the R accumulators, each product beside its add) instead of hoisting products or loads; the
+    // LDS reads are software-pipelined by hand: tap rows FE_PF samples ahead, chunks 2 ahead.
+#pragma unroll
+    for (int S = TWIN - 1; S >= 0; S--) {
+        const int slot = S % FE_PF;
+        if (((S & 7) == 7 || S == TWIN - 1) && (S >> 3) >= 2) chunk[(S >> 3) - 2] = tw[(S >> 3) - 2];
+        const uint4 c4 = chunk[S >> 3];
+        const int dw = (S & 7) >> 1;
+        const uint32_t w = (dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w) ^ 0x80808080u;
+        const int sh = (S & 1) * 16;
+        const f32x2 m = f32x2{(float)(int8_t)((w >> sh) & 0xFFu), (float)(int8_t)((w >> (sh + 8)) & 0xFFu)};
+        float tap[R];
+#pragma unroll
+        for (int q = 0; q < R / 4; q++) {
+            tap[4 * q] = ring[slot][q].x; tap[4 * q + 1] = ring[slot][q].y;
+            tap[4 * q + 2] = ring[slot][q].z; tap[4 * q + 3] = ring[slot][q].w;
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int k = r * D + HP - S;
+            if (k >= 0 && k < NT) {
+                const float hk = tap[r];
+                if (FAST) acc[r] = __builtin_elementwise_fma(f32x2{hk, hk}, m, acc[r]);
+                else acc[r] = acc[r] + f32x2{hk, hk} * m;
+            }
+        }
+        if (S - FE_PF >= 0) {
+#pragma unroll
+            for (int q = 0; q < R / 4; q++) ring[slot][q] = tt4[(S - FE_PF) * (R / 4) + q];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- discriminator (demod.cpp:8-19); the previous output of lane t's first comes from lane t-1
+    const f32x2 left = f32x2{__shfl_up(acc[R - 1].x, 1), __shfl_up(acc[R - 1].y, 1)};
+    float* out = fm + (size_t)ch * fm_stride;
+    const int cbase = c0 + t * R;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int c = cbase + r;
+        f32x2 pv = (r > 0) ? acc[r > 0 ? r - 1 : 0] : left;
+        if (c == 0) {
+            const float2 p = prev_in[ch];
+            pv = f32x2{p.x, p.y};
+        }
+        const f32x2 cur = acc[r];
+        float v;
+        if ((cur.x == 0) & (cur.y == 0)) {
+            v = 0.0f;
+        } else {
+            const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
+            const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
+            v = (float)((double)num / den);
+        }
+        if (c > c0 && c >= 0 && c < block_if) out[c] = v;
+        if (c == block_if - 1) prev_out[ch] = make_float2(cur.x, cur.y);
+    }
+    if (blockIdx.x == 0) {
+        const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
+        uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
+        for (int i = t; i < HP; i += NTH) tout[i] = last[i];
+        const float* o = fm_other + (size_t)ch * fm_stride;
+        for (int i = t; i < HIST; i += NTH) out[i - HIST] = o[block_if - HIST + i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Decimating FIR, filter.cpp:106-121: y[n] = sum_{k<ntaps} h[k] * x[nD-k], ascending k, f32
 // mul then add. x[m] for m < 0 comes from `hist` (hist[m], m >= -nhist). NT = 1 or 2 tap sets
 // sharing one staged window. SQUARE: the input is x*x (rds.cpp:111-113 fused into :116).
@@ -759,7 +920,7 @@ struct sdr_ctx {
     sdr_info info{};
     int ntaps = 101;
     // taps (device)
-    float *rf_h = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
+    float *rf_h = nullptr, *rf_hs = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
           *rrc_h = nullptr;
     float *audio_pp = nullptr, *rdsbb_pp = nullptr;   // polyphase tables
     int *audio_cnt = nullptr, *rdsbb_cnt = nullptr;
@@ -903,6 +1064,18 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     c->rdsbb_L = pr.L;
 #define TRY(x) do { int r_ = (x); if (r_) { sdr_ctx_destroy(c); return r_; } } while (0)
     TRY(upload(c, &c->rf_h, rf));
+    {
+        // front-end v2 tap table: row S (input sample S of a thread window, R = 8 outputs) holds
+        // h[r*D + 100 - S] / 128 (exact power-of-two scaling) or 0 where that tap does not exist
+        const int R = 8, D = in.rf_decim, TWIN = (R - 1) * D + T;
+        std::vector<float> tt((size_t)TWIN * R, 0.0f);
+        for (int S_ = 0; S_ < TWIN; S_++)
+            for (int r = 0; r < R; r++) {
+                const int k = r * D + (T - 1) - S_;
+                if (k >= 0 && k < T) tt[(size_t)S_ * R + r] = rf[k] * 0.0078125f;
+            }
+        TRY(upload(c, &c->rf_hs, tt));
+    }
     TRY(upload(c, &c->pilot_h, pilot));
     TRY(upload(c, &c->stereo_h, stereo));
     TRY(upload(c, &c->rds_h, rds));
@@ -976,12 +1149,29 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     uint8_t* tail_out = c->tail + (size_t)p * c->nch * 2 * hp;
     const float2* prev_in = c->prev + (size_t)(p ^ 1) * c->nch;
     float2* prev_out = c->prev + (size_t)p * c->nch;
-    const int tile = FIR_TILE;
-    dim3 grid(cdiv(in.block_if, tile), c->nch);
-    const size_t lds = frontend_lds_bytes(c->ntaps, tile, in.rf_decim);
-    hipLaunchKernelGGL(k_frontend, grid, dim3(BLK), lds, S(stream), iq, iq_stride, tail_in, tail_out, prev_in,
-                       prev_out, c->rf_h, c->ntaps, in.rf_decim, in.block_iq, in.block_if, tile,
-                       c->fm + p * c->fm_par, c->fm + (p ^ 1) * c->fm_par, c->fm_stride);
+    const bool fast = (c->flags & SDR_FLAG_FAST_FRONTEND) != 0;
+    float* fm_p = c->fm + p * c->fm_par;
+    const float* fm_o = c->fm + (p ^ 1) * c->fm_par;
+    constexpr int R = 8;
+    const dim3 g2(cdiv(in.block_if + 1, 64 * R - 1), c->nch);
+#define FE2(DD, FF)                                                                                          \
+    hipLaunchKernelGGL((k_frontend2<R, DD, FF>), g2, dim3(64), 0, S(stream), iq, iq_stride, tail_in, tail_out,   \
+                       prev_in, prev_out, c->rf_hs, in.block_iq, in.block_if, fm_p, fm_o, c->fm_stride)
+    if (c->ntaps == 101 && in.rf_decim == 10) {
+        if (fast) FE2(10, true); else FE2(10, false);
+    } else if (c->ntaps == 101 && in.rf_decim == 4) {
+        if (fast) FE2(4, true); else FE2(4, false);
+    } else if (c->ntaps == 101 && in.rf_decim == 3) {
+        if (fast) FE2(3, true); else FE2(3, false);
+    } else {
+        const int tile = FIR_TILE;
+        dim3 grid(cdiv(in.block_if, tile), c->nch);
+        const size_t lds = frontend_lds_bytes(c->ntaps, tile, in.rf_decim);
+        hipLaunchKernelGGL(k_frontend, grid, dim3(BLK), lds, S(stream), iq, iq_stride, tail_in, tail_out, prev_in,
+                           prev_out, c->rf_h, c->ntaps, in.rf_decim, in.block_iq, in.block_if, tile, fm_p, fm_o,
+                           c->fm_stride);
+    }
+#undef FE2
     LAUNCH_CHECK();
     c->parity = p;
     c->block++;

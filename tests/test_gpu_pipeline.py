@@ -164,3 +164,22 @@ def test_fast_pll_matches_libm_pll(pkg, synth, torch_cuda):
         assert torch.equal(pa.nbits, pb.nbits) and torch.equal(pa.bits, pb.bits)
     pa.close()
     pb.close()
+
+
+def test_fast_frontend_tolerance_and_rds_bits(pkg, synth, golden_long, oracle, torch_cuda):
+    """SDR_FLAG_FAST_FRONTEND (v_pk_fma_f32 FIR): fm_demod within 1e-5 relative (north-star
+    tolerance; measured ~1e-7) of the reference, and the RDS bit decisions of the 200-block
+    golden run still bit-exact."""
+    nb = golden_long["nblocks"]
+    chans = [int(c) for c in golden_long["channels"]]
+    iqs = [channel_input(synth, c, nb, golden_long["channels"][str(c)]["input_sha256"]) for c in chans]
+    out = _run_pipeline(pkg, torch_cuda, iqs, nb, flags=pkg.FLAG_FAST_FRONTEND)
+    ref = oracle.run_channel(iqs[0][:8], 0, True)
+    for b in range(8):
+        got, want = out["fm"][b][0].astype(np.float64), ref["fm_demod"][b].astype(np.float64)
+        scale = np.max(np.abs(want))
+        assert np.max(np.abs(got - want)) <= 1e-5 * scale, f"fm_demod block {b}"
+    for j, c in enumerate(chans):
+        for b, want in enumerate(golden_long["channels"][str(c)]["blocks"]):
+            if "bits" in want:
+                assert _bitstr(out["bits"][b][j], int(out["nbits"][b][j])) == want["bits"], f"bits ch{c} block {b}"
