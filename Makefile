@@ -1,7 +1,10 @@
 # Build everything in-tree (the .so files travel to the GPU box with the snapshot).
-#   make            libsdr_amd.so (HIP, gfx950) + oracle/liboracle.so (+ oracle/_ref when the
-#                   reference tree is present in this container)
+#   make            libsdr_amd.so (HIP kernels + C ABI, gfx950), libsdr_host.so (the reference's
+#                   C++ stage/primitive API over the C ABI), bin/sdr_project (the receiver CLI),
+#                   oracle/liboracle.so (+ oracle/_ref when the reference tree is present here)
 HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ROCM     ?= /opt/rocm
 ARCH     ?= gfx950
 PKG      := real-time-sdr_amd
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-flush-denormals-to-zero \
@@ -9,19 +12,36 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-g
             -Wall -Iinclude
 LIB      := $(PKG)/libsdr_amd.so
 SRCS     := $(PKG)/csrc/sdr_kernels.hip $(PKG)/csrc/sdr_taps.cpp
-HDRS     := include/sdr_amd.h
+HDRS     := include/sdr_amd.h $(PKG)/csrc/pll_math.h
 
-.PHONY: all lib oracle clean
-all: lib oracle
+# host C++ (no device code): compiled by the system g++ against the HIP runtime headers
+HOSTFLAGS := -O2 -std=c++17 -fPIC -Wall -Wextra -pthread -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include \
+             -Iinclude -Iinclude/dropin -I$(PKG)/host
+HOSTLIB   := $(PKG)/libsdr_host.so
+HOSTSRCS  := $(PKG)/host/dropin_primitives.cpp $(PKG)/host/dropin_stages.cpp $(PKG)/host/rds_frame.cpp
+HOSTHDRS  := $(wildcard include/dropin/*.h) $(PKG)/host/hip_util.h include/sdr_amd.h
+CLI       := $(PKG)/bin/sdr_project
+
+.PHONY: all lib host oracle clean
+all: lib host oracle
 
 lib: $(LIB)
+host: $(HOSTLIB) $(CLI)
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
 
-oracle:
+$(HOSTLIB): $(HOSTSRCS) $(HOSTHDRS) $(LIB)
+	$(CXX) $(HOSTFLAGS) -shared -o $@ $(HOSTSRCS) -L$(PKG) -lsdr_amd -L$(ROCM)/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(ROCM)/lib
+
+$(CLI): $(PKG)/host/sdr_project.cpp $(HOSTLIB)
+	@mkdir -p $(dir $@)
+	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -lsdr_host -Wl,-rpath,'$$ORIGIN/..'
+
+oracle: host
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIB)
+	rm -f $(LIB) $(HOSTLIB) $(CLI)
 	$(MAKE) -C oracle clean

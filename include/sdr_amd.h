@@ -95,6 +95,17 @@ int sdr_fmpll(float *out, size_t out_stride, const float *in, size_t in_stride, 
               void *stream);
 /* cdr(sps, signal): rds_utilities.cpp:4-21 (include/rds_utilities.h:6). offset: [nch] int32. */
 int sdr_cdr(int32_t *offset, const float *x, size_t x_stride, int nch, int n, int sps, void *stream);
+/* manchester_decode(bits, symbols, block_count, half_symbol, start): rds_utilities.cpp:34-68
+ * (include/rds_utilities.h:12). symbols [nch][sym_stride] 0/1 bytes with nsym[ch] valid;
+ * state [nch][2] = {half_symbol, start} updated in place; bits [nch][bits_stride] 0/1 bytes,
+ * nbits[ch] written. block_count as in the reference (0 selects the alignment search). */
+int sdr_manchester_decode(uint8_t *bits, size_t bits_stride, int32_t *nbits, const uint8_t *symbols,
+                          size_t sym_stride, const int32_t *nsym, int nch, int block_count, int32_t *state,
+                          void *stream);
+/* differential_decode(out, bits, last_bit, block_num): rds_utilities.cpp:70-88
+ * (include/rds_utilities.h:14). last_bit [nch] int32 updated in place. */
+int sdr_differential_decode(uint8_t *out, size_t out_stride, const uint8_t *bits, size_t bits_stride,
+                            const int32_t *nbits, int nch, int block_num, int32_t *last_bit, void *stream);
 
 /* ------------------------------------------------------------------ fused pipeline
  * A context owns the taps, every inter-stage buffer and all per-channel state of `nch`
@@ -119,6 +130,10 @@ int sdr_rds_dsp(sdr_ctx *ctx, float *rds_clean, size_t rds_stride, void *stream)
  * blocks that do not decode. Any output pointer may be NULL. Strides in elements. */
 int sdr_rds_bits(sdr_ctx *ctx, int32_t *offset, int32_t *nsym, uint8_t *symbols, size_t sym_stride,
                  int32_t *nbits, uint8_t *bits, size_t bits_stride, void *stream);
+/* Consumer-side entry (wait_and_pop, threadsafequeue.h:46): make an fm_demod block produced
+ * elsewhere (another context, another GPU, or host data copied to the device) the context's
+ * current block; mono/stereo/rds then consume it. fm [nch][block_if] device memory. */
+int sdr_push_fm_demod(sdr_ctx *ctx, const float *fm, size_t fm_stride, void *stream);
 /* Copy out the context's current-block fm_demod [nch][block_if] (the reference's queue payload) */
 int sdr_get_fm_demod(sdr_ctx *ctx, float *fm, size_t fm_stride, void *stream);
 /* Debug / parity access to intermediates of the current block (device pointers into the

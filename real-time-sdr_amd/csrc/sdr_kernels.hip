@@ -827,6 +827,52 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
     }
 }
 
+// manchester_decode (rds_utilities.cpp:34-68), one lane per channel
+__global__ void k_manchester(uint8_t* __restrict__ bits, size_t bits_stride, int32_t* __restrict__ nbits,
+                             const uint8_t* __restrict__ symbols, size_t sym_stride,
+                             const int32_t* __restrict__ nsym, int nch, int block_count,
+                             int32_t* __restrict__ state) {
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= nch) return;
+    const uint8_t* sy = symbols + (size_t)ch * sym_stride;
+    uint8_t* bo = bits + (size_t)ch * bits_stride;
+    const int m = nsym[ch];
+    int half_symbol = state[2 * ch], start = state[2 * ch + 1];
+    int nb = 0;
+    if (start) bo[nb++] = (uint8_t)half_symbol;
+    if (block_count == 0) {
+        int score = 0;
+        for (int i = 0; i < m - 1; i += 2) score += sy[i] ^ sy[i + 1];
+        for (int j = 1; j < m - 1; j += 2) score -= sy[j] ^ sy[j + 1];
+        start = score < 0;
+    }
+    for (int i = start; i < m - 1; i += 2) bo[nb++] = sy[i];
+    if (((m - start) & 0x01) == 1) {
+        half_symbol = sy[m - 1];
+        start = 1;
+    } else {
+        start = 0;
+    }
+    state[2 * ch] = half_symbol;
+    state[2 * ch + 1] = start;
+    nbits[ch] = nb;
+}
+
+// differential_decode (rds_utilities.cpp:70-88), one lane per channel
+__global__ void k_differential(uint8_t* __restrict__ out, size_t out_stride, const uint8_t* __restrict__ bits,
+                               size_t bits_stride, const int32_t* __restrict__ nbits, int nch, int block_num,
+                               int32_t* __restrict__ last_bit) {
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= nch) return;
+    const int nb = nbits[ch];
+    if (nb <= 0) return;
+    const uint8_t* b = bits + (size_t)ch * bits_stride;
+    uint8_t* o = out + (size_t)ch * out_stride;
+    o[0] = (block_num == 0) ? b[0] : (uint8_t)(b[0] ^ (uint8_t)last_bit[ch]);
+    for (int i = 1; i < nb; i++) o[i] = b[i] ^ b[i - 1];
+    last_bit[ch] = b[nb - 1];
+}
+
 __global__ void k_fill_u8(uint8_t* p, uint8_t v, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -1440,4 +1486,38 @@ int sdr_cdr(int32_t* offset, const float* x, size_t x_stride, int nch, int n, in
     return SDR_OK;
 }
 
+int sdr_manchester_decode(uint8_t* bits, size_t bits_stride, int32_t* nbits, const uint8_t* symbols, size_t sym_stride,
+                          const int32_t* nsym, int nch, int block_count, int32_t* state, void* stream) {
+    if (!bits || !nbits || !symbols || !nsym || !state || nch <= 0) return fail(SDR_E_INVALID, "manchester: bad arguments");
+    hipLaunchKernelGGL(k_manchester, dim3(cdiv(nch, 64)), dim3(64), 0, S(stream), bits, bits_stride, nbits, symbols,
+                       sym_stride, nsym, nch, block_count, state);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+int sdr_differential_decode(uint8_t* out, size_t out_stride, const uint8_t* bits, size_t bits_stride,
+                            const int32_t* nbits, int nch, int block_num, int32_t* last_bit, void* stream) {
+    if (!out || !bits || !nbits || !last_bit || nch <= 0) return fail(SDR_E_INVALID, "differential: bad arguments");
+    hipLaunchKernelGGL(k_differential, dim3(cdiv(nch, 64)), dim3(64), 0, S(stream), out, out_stride, bits, bits_stride,
+                       nbits, nch, block_num, last_bit);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+int sdr_push_fm_demod(sdr_ctx* c, const float* fm, size_t fm_stride, void* stream) {
+    if (!c || !fm) return fail(SDR_E_INVALID, "null argument");
+    const sdr_info& in = c->info;
+    const int p = c->parity ^ 1;
+    float* dst = c->fm + p * c->fm_par;
+    HIP_TRY(hipMemcpy2DAsync(dst, c->fm_stride * sizeof(float), fm, fm_stride * sizeof(float),
+                             in.block_if * sizeof(float), c->nch, hipMemcpyDeviceToDevice, S(stream)));
+    hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, S(stream), dst, c->fm + (p ^ 1) * c->fm_par,
+                       c->fm_stride, in.block_if);
+    LAUNCH_CHECK();
+    c->parity = p;
+    c->block++;
+    return SDR_OK;
+}
+
 }  // extern "C"
+
