@@ -1407,16 +1407,22 @@ int sdr_convolve_fir(float* y, size_t y_stride, const float* x, size_t x_stride,
 }
 
 namespace {
-struct PPCache {
-    std::mutex m;
-    const float* h = nullptr;
-    int ntaps = 0, U = 0;
+// polyphase tables of the taps the primitive resampler has been called with, keyed by (U, tap
+// values): the reference's callers use a few fixed filters, so entries are kept (never freed
+// under a kernel still in flight) and the set is only dropped, after a device sync, if it grows
+struct PPEntry {
+    int U = 0;
     std::vector<float> host;
     float* table = nullptr;
     int* cnt = nullptr;
     int L = 0;
 };
+struct PPCache {
+    std::mutex m;
+    std::vector<PPEntry> e;
+};
 PPCache g_pp;
+constexpr size_t PP_CACHE_MAX = 16;
 }  // namespace
 
 int sdr_convolve_fir_resample(float* y, size_t y_stride, const float* x, size_t x_stride, int nch, int nx,
@@ -1424,19 +1430,30 @@ int sdr_convolve_fir_resample(float* y, size_t y_stride, const float* x, size_t 
     if (!y || !x || !h || !state || nch <= 0 || nx <= 0 || ntaps <= 0 || U <= 0 || D <= 0)
         return fail(SDR_E_INVALID, "convolve_fir_resample: bad arguments");
     const int ny = (int)(((long long)nx * U) / D);
-    // polyphase table of the (device) taps, cached per (h, ntaps, U)
-    std::lock_guard<std::mutex> lk(g_pp.m);
+    // polyphase table of the (device) taps; the taps are read on the caller's stream so that a
+    // preceding asynchronous upload of them on that stream is complete
     std::vector<float> hh(ntaps);
-    HIP_TRY(hipMemcpy(hh.data(), h, ntaps * sizeof(float), hipMemcpyDeviceToHost));
-    if (g_pp.h != h || g_pp.ntaps != ntaps || g_pp.U != U || g_pp.host != hh) {
-        if (g_pp.table) (void)hipFree(g_pp.table);
-        if (g_pp.cnt) (void)hipFree(g_pp.cnt);
+    HIP_TRY(hipMemcpyAsync(hh.data(), h, ntaps * sizeof(float), hipMemcpyDeviceToHost, S(stream)));
+    HIP_TRY(hipStreamSynchronize(S(stream)));
+    std::lock_guard<std::mutex> lk(g_pp.m);
+    const PPEntry* pe = nullptr;
+    for (const PPEntry& e : g_pp.e)
+        if (e.U == U && e.host == hh) { pe = &e; break; }
+    if (!pe) {
+        if (g_pp.e.size() >= PP_CACHE_MAX) {
+            HIP_TRY(hipDeviceSynchronize());
+            for (PPEntry& e : g_pp.e) { (void)hipFree(e.table); (void)hipFree(e.cnt); }
+            g_pp.e.clear();
+        }
         Polyphase pp = make_polyphase(hh, U);
-        HIP_TRY(hipMalloc(&g_pp.table, pp.table.size() * sizeof(float)));
-        HIP_TRY(hipMalloc(&g_pp.cnt, pp.cnt.size() * sizeof(int)));
-        HIP_TRY(hipMemcpy(g_pp.table, pp.table.data(), pp.table.size() * sizeof(float), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(g_pp.cnt, pp.cnt.data(), pp.cnt.size() * sizeof(int), hipMemcpyHostToDevice));
-        g_pp.h = h; g_pp.ntaps = ntaps; g_pp.U = U; g_pp.host = hh; g_pp.L = pp.L;
+        PPEntry ne;
+        ne.U = U; ne.host = hh; ne.L = pp.L;
+        HIP_TRY(hipMalloc(&ne.table, pp.table.size() * sizeof(float)));
+        HIP_TRY(hipMalloc(&ne.cnt, pp.cnt.size() * sizeof(int)));
+        HIP_TRY(hipMemcpy(ne.table, pp.table.data(), pp.table.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(ne.cnt, pp.cnt.data(), pp.cnt.size() * sizeof(int), hipMemcpyHostToDevice));
+        g_pp.e.push_back(std::move(ne));
+        pe = &g_pp.e.back();
     }
     // the deepest look-back is output 0: x[-(ceil(ntaps/U)-1)] (100 in every mode)
     const int lookback = (ntaps + U - 1) / U - 1;
@@ -1444,10 +1461,10 @@ int sdr_convolve_fir_resample(float* y, size_t y_stride, const float* x, size_t 
         return fail(SDR_E_INVALID, "convolve_fir_resample: nstate %d < look-back %d", nstate, lookback);
     if (ny > 0) {
         const int tile = 256;
-        const size_t lds = resample_lds_bytes(g_pp.L, U, D, tile, 1);
+        const size_t lds = resample_lds_bytes(pe->L, U, D, tile, 1);
         hipLaunchKernelGGL(k_resample<0>, dim3(cdiv(ny, tile), nch), dim3(BLK), lds, S(stream), x, state + nstate,
-                           x_stride, (size_t)nstate, nullptr, nullptr, (size_t)0, (size_t)0, g_pp.table, g_pp.cnt,
-                           g_pp.L, U, D, ny, tile, -nstate, (void*)y, y_stride);
+                           x_stride, (size_t)nstate, nullptr, nullptr, (size_t)0, (size_t)0, pe->table, pe->cnt,
+                           pe->L, U, D, ny, tile, -nstate, (void*)y, y_stride);
         LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_state_update, dim3(nch), dim3(256), 0, S(stream), state, nstate, x, x_stride, nx);
