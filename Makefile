@@ -29,7 +29,7 @@ lib: $(LIB)
 host: $(HOSTLIB) $(CLI)
 
 $(LIB): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,libsdr_amd.so -o $@ $(SRCS)
 
 $(HOSTLIB): $(HOSTSRCS) $(HOSTHDRS) $(LIB)
 	$(CXX) $(HOSTFLAGS) -shared -o $@ $(HOSTSRCS) -L$(PKG) -lsdr_amd -L$(ROCM)/lib -lamdhip64 \

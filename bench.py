@@ -149,7 +149,9 @@ def main() -> None:
 
     nch = args.channels
     nblocks = args.warmup + args.steps
-    iq = make_input(torch, nch, nblocks, first_channel=rank * nch, device=dev)
+    from real_time_sdr_amd.sharding import channel_range
+    first, nch = channel_range(nch, rank)
+    iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
     pipe = pkg.Pipeline(nch, mode=0, rds_on=True, device=local)
     info = pipe.info
     s_rf, s_au, s_rds = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
@@ -162,10 +164,11 @@ def main() -> None:
     done_au = [ev() for _ in range(nblocks)]
     done_rds = [ev() for _ in range(nblocks)]
     done_rf = [ev() for _ in range(nblocks)]
-    gather_bufs = None
+    gather = None
     if world > 1 and not args.no_gather:
-        gather_bufs = (torch.empty(world * nch, 2 * info.n_audio, dtype=torch.int16, device=dev),
-                       torch.empty(world * nch, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev))
+        from real_time_sdr_amd.sharding import BlockGather
+        gather = BlockGather(torch, dist, world, {"lr": ((nch, 2 * info.n_audio), torch.int16),
+                                                  "bits": ((nch, pkg.SDR_MAX_BITS), torch.uint8)}, dev)
 
     def step(b: int) -> None:
         # front end (producer): may overwrite the fm_demod parity of block b-2 only after both
@@ -186,13 +189,12 @@ def main() -> None:
         s_rds.wait_event(done_rf[b])
         pipe.rds(clean, stream=s_rds)
         done_rds[b].record(s_rds)
-        if gather_bufs is not None:
+        if gather is not None:
             # final audio / bitstream gather over RCCL (xGMI) on the default stream
             cur = torch.cuda.current_stream(dev)
             cur.wait_event(done_au[b])
             cur.wait_event(done_rds[b])
-            dist.all_gather_into_tensor(gather_bufs[0], lr)
-            dist.all_gather_into_tensor(gather_bufs[1], pipe.bits)
+            gather.gather(lr=lr, bits=pipe.bits)
 
     for b in range(args.warmup):
         step(b)
@@ -209,9 +211,8 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from real_time_sdr_amd.sharding import max_over_ranks
+        elapsed = max_over_ranks(torch, dist, elapsed, dev)
 
     # front-end kernel (FIR /10 + discriminator) duration from HIP events on its own stream
     fe_ms = [fe_start[b].elapsed_time(fe_end[b]) for b in range(args.warmup, nblocks)]
