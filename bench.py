@@ -154,16 +154,19 @@ def main() -> None:
     iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
     pipe = pkg.Pipeline(nch, mode=0, rds_on=True, device=local)
     info = pipe.info
-    s_rf, s_au, s_rds = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    # Three streams, one HIP hardware queue each (GPU_MAX_HW_QUEUES is 4 and one serves the null
+    # stream; a fourth stream would share a queue and serialise behind it): front end + mono + the
+    # FIRs feeding both PLLs; both PLLs in one dispatch; everything after the PLLs. The serial PLLs
+    # bound the step, so they run back to back across blocks while the other streams fill the chip.
+    s_fe, s_pll, s_post = (torch.cuda.Stream(dev) for _ in range(3))
     mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
-    lr = torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev)
+    lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]
+    bits = [torch.empty(nch, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev) for _ in range(2)]
     clean = torch.empty(nch, info.n_rds, dtype=torch.float32, device=dev)
     ev = lambda: torch.cuda.Event(enable_timing=False)  # noqa: E731
     fe_start = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
     fe_end = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
-    done_au = [ev() for _ in range(nblocks)]
-    done_rds = [ev() for _ in range(nblocks)]
-    done_rf = [ev() for _ in range(nblocks)]
+    pre_done, pll_done, post_done, gather_done = ([ev() for _ in range(nblocks)] for _ in range(4))
     gather = None
     if world > 1 and not args.no_gather:
         from real_time_sdr_amd.sharding import BlockGather
@@ -171,30 +174,34 @@ def main() -> None:
                                                   "bits": ((nch, pkg.SDR_MAX_BITS), torch.uint8)}, dev)
 
     def step(b: int) -> None:
-        # front end (producer): may overwrite the fm_demod parity of block b-2 only after both
-        # consumers released it (threadsafequeue.h:29-31)
+        # the front end of block b reuses block b-2's parity: both consumers must have released it
+        # (threadsafequeue.h:29-31), i.e. block b-2's post-PLL work is done
         if b >= 2:
-            s_rf.wait_event(done_au[b - 2])
-            s_rf.wait_event(done_rds[b - 2])
-        fe_start[b].record(s_rf)
-        pipe.frontend(iq[b], stream=s_rf)
-        fe_end[b].record(s_rf)
-        done_rf[b].record(s_rf)
-        # audio consumer: mono + stereo (mono.cpp, stereo.cpp)
-        s_au.wait_event(done_rf[b])
-        pipe.mono(mono, stream=s_au)
-        pipe.stereo(lr, stream=s_au)
-        done_au[b].record(s_au)
-        # RDS consumer: DSP + bits (rds.cpp)
-        s_rds.wait_event(done_rf[b])
-        pipe.rds(clean, stream=s_rds)
-        done_rds[b].record(s_rds)
+            s_fe.wait_event(post_done[b - 2])
+        fe_start[b].record(s_fe)
+        pipe.frontend(iq[b], stream=s_fe)                # rffrontend.cpp:58-71
+        fe_end[b].record(s_fe)
+        pipe.mono(mono, stream=s_fe)                     # mono.cpp:34-42
+        pipe.stereo_pre(stream=s_fe)                     # stereo.cpp:74, :80
+        pipe.rds_pre(stream=s_fe)                        # rds.cpp:105-116
+        pre_done[b].record(s_fe)
+        s_pll.wait_event(pre_done[b])
+        pipe.plls(stream=s_pll)                          # stereo.cpp:77 + rds.cpp:119
+        pll_done[b].record(s_pll)
+        s_post.wait_event(pll_done[b])
+        if gather is not None and b >= 2:
+            s_post.wait_event(gather_done[b - 2])        # lr/bits slot of block b-2 gathered
+        pipe.stereo_post(lr[b % 2], stream=s_post)       # stereo.cpp:83-107
+        pipe.rds_post(clean, bits=True, stream=s_post)   # rds.cpp:122-167
+        with torch.cuda.stream(s_post):
+            bits[b % 2].copy_(pipe.bits)
+        post_done[b].record(s_post)
         if gather is not None:
-            # final audio / bitstream gather over RCCL (xGMI) on the default stream
+            # final audio / bitstream gather over RCCL (xGMI)
             cur = torch.cuda.current_stream(dev)
-            cur.wait_event(done_au[b])
-            cur.wait_event(done_rds[b])
-            gather.gather(lr=lr, bits=pipe.bits)
+            cur.wait_event(post_done[b])
+            gather.gather(lr=lr[b % 2], bits=bits[b % 2])
+            gather_done[b].record(cur)
 
     for b in range(args.warmup):
         step(b)

@@ -125,6 +125,25 @@ int sdr_mono(sdr_ctx *ctx, int16_t *audio, size_t audio_stride, void *stream);
 int sdr_stereo(sdr_ctx *ctx, int16_t *lr, size_t lr_stride, void *stream);
 /* rds DSP (rds.cpp:105-133): rds_clean [nch][n_rds] f32 (may be NULL: kept internally) */
 int sdr_rds_dsp(sdr_ctx *ctx, float *rds_clean, size_t rds_stride, void *stream);
+/* The same two loop bodies split at their PLL, in this order per block (each part may run on its
+ * own stream; the caller orders them with events): sdr_X = sdr_X_pre; sdr_X_pll; sdr_X_post.
+ *   stereo_pre   pilot + band BPFs          stereo.cpp:74, :80
+ *   stereo_pll   19 kHz PLL, x2 carrier      stereo.cpp:77
+ *   stereo_post  mixer, delay, resamplers    stereo.cpp:83-107
+ *   rds_pre      BPF, squaring, 114 kHz BPF  rds.cpp:105-116
+ *   rds_pll      114 kHz PLL, x0.5           rds.cpp:119
+ *   rds_post     delay, mixer, 247/640, RRC  rds.cpp:122-133
+ * Intermediates crossing the split are kept per block parity, so the PLL of block b+1 may run
+ * while block b's post part is still running. */
+int sdr_stereo_pre(sdr_ctx *ctx, void *stream);
+int sdr_stereo_pll(sdr_ctx *ctx, void *stream);
+int sdr_stereo_post(sdr_ctx *ctx, int16_t *lr, size_t lr_stride, void *stream);
+int sdr_rds_pre(sdr_ctx *ctx, void *stream);
+int sdr_rds_pll(sdr_ctx *ctx, void *stream);
+int sdr_rds_post(sdr_ctx *ctx, float *rds_clean, size_t rds_stride, void *stream);
+/* stereo_pll + rds_pll of the current block in one dispatch (2 x nch independent recurrences);
+ * needs both _pre parts done. */
+int sdr_plls(sdr_ctx *ctx, void *stream);
 /* rds symbol/bit recovery (rds.cpp:135-167): per channel, for blocks with block_count > 5 and
  * rds_on: offset = cdr(), symbols (0/1 bytes), bits (decoded 0/1 bytes). nbits[ch] = -1 on
  * blocks that do not decode. Any output pointer may be NULL. Strides in elements. */

@@ -80,6 +80,14 @@ def lib() -> C.CDLL:
         "sdr_rds_dsp": ([vp, vp, sz, vp], i32),
         "sdr_rds_bits": ([vp, vp, vp, vp, sz, vp, vp, sz, vp], i32),
         "sdr_get_fm_demod": ([vp, vp, sz, vp], i32),
+        "sdr_push_fm_demod": ([vp, vp, sz, vp], i32),
+        "sdr_stereo_pre": ([vp, vp], i32),
+        "sdr_stereo_pll": ([vp, vp], i32),
+        "sdr_stereo_post": ([vp, vp, sz, vp], i32),
+        "sdr_rds_pre": ([vp, vp], i32),
+        "sdr_rds_pll": ([vp, vp], i32),
+        "sdr_plls": ([vp, vp], i32),
+        "sdr_rds_post": ([vp, vp, sz, vp], i32),
         "sdr_ctx_buffer": ([vp, C.c_char_p, C.POINTER(vp), C.POINTER(sz), C.POINTER(i32)], i32),
     }
     for name, (args, res) in sigs.items():
@@ -271,6 +279,42 @@ class Pipeline:
             out = torch.empty(self.nch, 2 * self.info.n_audio, dtype=torch.int16, device=self.torch_device)
         check(lib().sdr_stereo(self._h, _ptr(out), _row_stride(out), _stream(stream)), "sdr_stereo")
         return out
+
+    # the stereo / RDS bodies split at their PLL (include/sdr_amd.h): pre; pll; post per block
+    def stereo_pre(self, stream=None):
+        check(lib().sdr_stereo_pre(self._h, _stream(stream)), "sdr_stereo_pre")
+
+    def stereo_pll(self, stream=None):
+        check(lib().sdr_stereo_pll(self._h, _stream(stream)), "sdr_stereo_pll")
+
+    def stereo_post(self, out, stream=None):
+        check(lib().sdr_stereo_post(self._h, _ptr(out), _row_stride(out), _stream(stream)), "sdr_stereo_post")
+        return out
+
+    def rds_pre(self, stream=None):
+        check(lib().sdr_rds_pre(self._h, _stream(stream)), "sdr_rds_pre")
+
+    def rds_pll(self, stream=None):
+        check(lib().sdr_rds_pll(self._h, _stream(stream)), "sdr_rds_pll")
+
+    def plls(self, stream=None):
+        """stereo_pll + rds_pll in one dispatch."""
+        check(lib().sdr_plls(self._h, _stream(stream)), "sdr_plls")
+
+    def rds_post(self, out=None, bits=True, stream=None):
+        check(lib().sdr_rds_post(self._h, _ptr(out), _row_stride(out) if out is not None else 0, _stream(stream)),
+              "sdr_rds_post")
+        if bits:
+            self.rds_bits(stream)
+        return out
+
+    def rds_bits(self, stream=None):
+        check(lib().sdr_rds_bits(self._h, _ptr(self.offset), _ptr(self.nsym), _ptr(self.symbols), SDR_MAX_SYMS,
+                                 _ptr(self.nbits), _ptr(self.bits), SDR_MAX_BITS, _stream(stream)), "sdr_rds_bits")
+
+    def push_fm_demod(self, fm, stream=None):
+        """Make fm [nch][block_if] (device f32) the current block (the queue's consumer side)."""
+        check(lib().sdr_push_fm_demod(self._h, _ptr(fm), _row_stride(fm), _stream(stream)), "sdr_push_fm_demod")
 
     def rds(self, out=None, bits=True, stream=None):
         """RDS DSP (+ symbol/bit recovery). Returns rds_clean [nch][n_rds]; bits in self.bits/nbits."""

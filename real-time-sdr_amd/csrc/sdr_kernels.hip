@@ -171,144 +171,248 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // sched_barrier closes every sample so the scheduler keeps the sample-major order (ILP across the
 // R accumulators, each product next to its add) instead of hoisting products or serialising one
 // output's chain; the LDS chunk two chunks ahead is read at each chunk boundary.
-constexpr int FE_PF = 3;   // tap rows prefetched this many samples ahead (rotating register ring)
+constexpr int FE_PF = 3;   // tap rows prefetched this many samples ahead (rotating SGPR ring)
 
+// {h, h} * m with h one half (HI) of an SGPR pair: v_pk_mul_f32 with a scalar operand whose half
+// is broadcast to both lanes by op_sel / op_sel_hi (no VGPR copy of the tap)
+__device__ __forceinline__ f32x2 fe_mul_v(double hpair, int hi, f32x2 m) {
+    f32x2 r;
+    if (hi) asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "s"(hpair), "v"(m));
+    else asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "s"(hpair), "v"(m));
+    return r;
+}
+// (I, Q) of one sample, sign-extended from the bytes of a dword that holds two samples
+// (u8 ^ 0x80 == u8 - 128 as int8), converted in program order (volatile asm)
+template <int HALF>
+__device__ __forceinline__ f32x2 fe_cvt_v(uint32_t w) {
+    f32x2 r;
+    if (HALF) {
+        asm volatile("v_cvt_f32_i32_sdwa %0, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2\n\t"
+                     "v_cvt_f32_i32_sdwa %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3"
+                     : "=&v"(r.x), "=v"(r.y) : "v"(w));
+    } else {
+        asm volatile("v_cvt_f32_i32_sdwa %0, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0\n\t"
+                     "v_cvt_f32_i32_sdwa %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1"
+                     : "=&v"(r.x), "=v"(r.y) : "v"(w));
+    }
+    return r;
+}
+__device__ __forceinline__ f32x2 fe_add_v(f32x2 a, f32x2 b) {
+    f32x2 r;
+    asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f32x2 fe_fma(double hpair, int hi, f32x2 m, f32x2 acc) {
+    f32x2 r;
+    if (hi) asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "=v"(r) : "s"(hpair), "v"(m), "v"(acc));
+    else asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "s"(hpair), "v"(m), "v"(acc));
+    return r;
+}
+
+// Persistent front end: each 64-lane workgroup walks tiles (channel-major, stride gridDim.x).
+// The next tile's u8 window is loaded into registers (coalesced dwords) while the current tile
+// computes out of LDS, then written to LDS -- global latency overlaps the FIR instead of
+// stalling every wave at its start. One tile = 64*R decimated outputs starting one before the
+// first fm_demod sample it writes (the discriminator's carry, demod.cpp:16); tiles advance by
+// 64*R-1. Boundary tiles (the first, which reads the previous block's tail, and the last, padded
+// with u8 128 = 0.0f) take a bytewise path.
 template <int R, int D, bool FAST>
 __global__ __launch_bounds__(64) void k_frontend2(
     const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
     uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
     const float* __restrict__ hs, int block_iq, int block_if,
-    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride) {
+    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int nch, int tiles_ch,
+    const uint32_t* __restrict__ pad) {
     constexpr int NT = 101, HP = NT - 1, NTH = 64;
     constexpr int TILE = NTH * R;
+    constexpr int ADV = TILE - 1;
     constexpr int WIN = (TILE - 1) * D + NT;          // staged samples (u8 I/Q pairs)
     constexpr int TWIN = (R - 1) * D + NT;            // samples one thread reads
     constexpr int TCH = (2 * TWIN + 15) / 16;         // 16-byte LDS chunks per thread window
+    constexpr int NG = (2 * WIN + 3) / 4;             // dwords of one tile window
+    constexpr int PER = (NG + NTH - 1) / NTH;         // dwords per lane
     constexpr int LDS_BYTES = ((2 * WIN + 15) / 16) * 16 + 32;
     __shared__ __attribute__((aligned(16))) uint8_t sw[LDS_BYTES];
-    __shared__ __attribute__((aligned(16))) float stt[TWIN * R];
-    const int ch = blockIdx.y, t = threadIdx.x;
-    for (int i = t; i < TWIN * R / 4; i += NTH)
-        reinterpret_cast<float4*>(stt)[i] = reinterpret_cast<const float4*>(hs)[i];
-    const int c0 = blockIdx.x * (TILE - 1) - 1;       // first decimated output (the carry)
-    const int m0 = c0 * D - HP;                       // first staged sample
-    const uint8_t* src = iq + (size_t)ch * iq_stride;
-    const uint8_t* tin = tail_in + (size_t)ch * 2 * HP;
-    const bool interior = (m0 >= 0) && (m0 + WIN <= block_iq);
-    // ---- stage the window ----
-    if (D % 2 == 0) {
-        constexpr int NG = (2 * WIN + 3) / 4;         // dword granules (2 samples each)
-        uint32_t* sd = reinterpret_cast<uint32_t*>(sw);
-        if (interior) {
+    const int t = threadIdx.x;
+    const int total = nch * tiles_ch;
+    int tile = blockIdx.x;
+    if (tile >= total) return;
+    uint32_t pf[PER];
+    bool pf_ok = true;
+    // window of tile `tl` -> pf (lane t holds dwords t, t+64, ...). Every I/Q sample is one u16;
+    // samples before the block come from the previous block's tail, samples past its end are
+    // u8 128 (== 0.0f). With D even the window starts on an even sample, so each dword is wholly
+    // in the block, in the tail or in the padding: one load (or constant) per dword on every tile.
+    auto fetch = [&](int tl) {
+        const int ch = tl / tiles_ch, j = tl - ch * tiles_ch;
+        const int m0 = (j * ADV - 1) * D - HP;
+        pf_ok = true;
+        const uint8_t* src = iq + (size_t)ch * iq_stride;
+        const uint8_t* tin = tail_in + (size_t)ch * 2 * HP;
+        if (D % 2 == 0) {
+            static_assert(D % 2 != 0 || D + HP < 2 * NTH, "boundary fetch assumes the tail lies in k == 0");
             const uint32_t* g = reinterpret_cast<const uint32_t*>(src + 2 * m0);
-#pragma unroll 8
-            for (int i = t; i < NG; i += NTH) sd[i] = g[i];
+            if (m0 >= 0 && m0 + WIN <= block_iq) {
+#pragma unroll
+                for (int k = 0; k < PER; k++) {
+                    const int i = t + NTH * k;
+                    pf[k] = (k < PER - 1 || i < NG) ? __builtin_nontemporal_load(g + i) : 0u;
+                }
+            } else {
+                pf_ok = false;   // boundary tile: staged straight into LDS when its turn comes
+            }
         } else {
-            for (int i = t; i < NG; i += NTH) {
+            const uint16_t* s16 = reinterpret_cast<const uint16_t*>(src);
+            const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tin);
+#pragma unroll
+            for (int k = 0; k < PER; k++) {
                 uint32_t v = 0;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    const int m = m0 + 2 * i + h;
-                    uint32_t pr = 0x8080u;   // outside the stream: u8 128 == 0.0f (zero state)
-                    if (m >= 0 && m < block_iq) pr = reinterpret_cast<const uint16_t*>(src)[m];
-                    else if (m < 0 && m >= -HP) pr = reinterpret_cast<const uint16_t*>(tin)[HP + m];
+                    const int m = m0 + 2 * (t + NTH * k) + h;
+                    const uint16_t* pa = m >= 0 ? s16 + m : t16 + (HP + m);
+                    if (m < -HP || m >= block_iq) pa = reinterpret_cast<const uint16_t*>(pad);
+                    const uint32_t pr = *pa;
                     v |= pr << (16 * h);
                 }
-                sd[i] = v;
+                pf[k] = v;
             }
         }
-    } else {
-        uint16_t* sh16 = reinterpret_cast<uint16_t*>(sw);
-        for (int i = t; i < WIN; i += NTH) {
-            const int m = m0 + i;
-            uint16_t pr = 0x8080u;
-            if (m >= 0 && m < block_iq) pr = reinterpret_cast<const uint16_t*>(src)[m];
-            else if (m < 0 && m >= -HP) pr = reinterpret_cast<const uint16_t*>(tin)[HP + m];
-            sh16[i] = pr;
+    };
+    fetch(tile);
+    while (tile < total) {
+        const int next = tile + (int)gridDim.x;
+        const int ch = tile / tiles_ch, j = tile - ch * tiles_ch;
+        const int c0 = j * ADV - 1;                   // first decimated output (the carry)
+        {
+            uint32_t* sd = reinterpret_cast<uint32_t*>(sw);
+            if (pf_ok) {
+#pragma unroll
+                for (int k = 0; k < PER; k++) {
+                    const int i = t + NTH * k;
+                    if (k < PER - 1 || i < NG) sd[i] = pf[k];
+                }
+            } else {
+                // boundary tile (D even): each dword lives wholly in the block, in the previous
+                // block's tail or in the padding (u8 128 == 0.0f); the address is chosen per dword
+                const int m0 = c0 * D - HP;
+                const uint32_t* gs = reinterpret_cast<const uint32_t*>(iq + (size_t)ch * iq_stride);
+                const uint32_t* gt = reinterpret_cast<const uint32_t*>(tail_in + (size_t)ch * 2 * HP);
+                for (int i = t; i < NG; i += NTH) {
+                    const int mm = m0 + 2 * i;
+                    const uint32_t* pa = mm >= 0 ? (mm < block_iq ? gs + (mm >> 1) : pad)
+                                                 : (mm >= -HP ? gt + ((HP + mm) >> 1) : pad);
+                    sd[i] = *pa;
+                }
+            }
         }
-    }
-    __syncthreads();
-    // ---- FIR: R outputs per thread, samples in descending order ----
-    uint4 chunk[TCH];
-    const uint4* tw = reinterpret_cast<const uint4*>(sw + 2 * t * R * D);
-    chunk[TCH - 1] = tw[TCH - 1];
-    if (TCH >= 2) chunk[TCH - 2] = tw[TCH - 2];
-    f32x2 acc[R];
+        __syncthreads();
+        if (next < total) fetch(next);                // in flight during the FIR
+        // ---- FIR: R outputs per thread, samples in descending order ----
+        uint4 chunk[TCH];
+        const uint4* tw = reinterpret_cast<const uint4*>(sw + 2 * t * R * D);
+        chunk[TCH - 1] = tw[TCH - 1];
+        if (TCH >= 2) chunk[TCH - 2] = tw[TCH - 2];
+        f32x2 acc[R];
 #pragma unroll
-    for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
-    const float4* tt4 = reinterpret_cast<const float4*>(stt);
-    float4 ring[FE_PF][R / 4];
+        for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
+        // Taps live in SGPRs: row S of the table holds the R taps sample S meets (uniform across
+        // the wave), fetched with scalar loads FE_PF samples ahead into a rotating ring and fed to
+        // the packed MACs as scalar operands (op_sel picks the half of the SGPR pair), so the VALU
+        // gets its taps without LDS or VGPR traffic.
+        // the tap pointer is made opaque per tile (otherwise every loop-invariant tap load is
+        // hoisted out of the tile loop and the 8*TWIN taps overflow the SGPR file), then declared
+        // uniform again with readfirstlane so the loads stay scalar
+        int zero = 0;
+        asm volatile("" : "+s"(zero));
+        zero = __builtin_amdgcn_readfirstlane(zero);
+        const double* hsd = reinterpret_cast<const double*>(hs) + zero;
+        double ring[FE_PF][R / 2];
 #pragma unroll
-    for (int j = 0; j < FE_PF; j++) {
-        const int S0 = TWIN - 1 - j;
+        for (int jj = 0; jj < FE_PF; jj++) {
+            const int S0 = TWIN - 1 - jj;
 #pragma unroll
-        for (int q = 0; q < R / 4; q++) ring[S0 % FE_PF][q] = tt4[S0 * (R / 4) + q];
-    }
-    // Samples in descending order, completely unrolled (the build raises clang's pragma-unroll
-    // threshold): chunk, tap-ring and accumulator indices are compile-time constants. A
-    // sched_barrier closes every sample so the scheduler keeps the sample-major order (ILP across
-    // the R accumulators, each product beside its add) instead of hoisting products or loads; the
-    // LDS reads are software-pipelined by hand: tap rows FE_PF samples ahead, chunks 2 ahead.
-#pragma unroll
-    for (int S = TWIN - 1; S >= 0; S--) {
-        const int slot = S % FE_PF;
-        if (((S & 7) == 7 || S == TWIN - 1) && (S >> 3) >= 2) chunk[(S >> 3) - 2] = tw[(S >> 3) - 2];
-        const uint4 c4 = chunk[S >> 3];
-        const int dw = (S & 7) >> 1;
-        const uint32_t w = (dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w) ^ 0x80808080u;
-        const int sh = (S & 1) * 16;
-        const f32x2 m = f32x2{(float)(int8_t)((w >> sh) & 0xFFu), (float)(int8_t)((w >> (sh + 8)) & 0xFFu)};
-        float tap[R];
-#pragma unroll
-        for (int q = 0; q < R / 4; q++) {
-            tap[4 * q] = ring[slot][q].x; tap[4 * q + 1] = ring[slot][q].y;
-            tap[4 * q + 2] = ring[slot][q].z; tap[4 * q + 3] = ring[slot][q].w;
+            for (int q = 0; q < R / 2; q++) ring[S0 % FE_PF][q] = hsd[S0 * (R / 2) + q];
         }
+        // sample S's (I, Q) as f32 (u8 - 128, exact) from the LDS chunk registers
+        auto sample = [&](int S) -> f32x2 {
+            const uint4 c4 = chunk[S >> 3];
+            const int dw = (S & 7) >> 1;
+            const uint32_t w = (dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w) ^ 0x80808080u;
+            return (S & 1) ? fe_cvt_v<1>(w) : fe_cvt_v<0>(w);
+        };
+        // one sample of look-ahead: sample S-1 is converted while sample S's MACs issue, so no MAC
+        // waits on its conversion
+        f32x2 m_next = sample(TWIN - 1);
+#pragma unroll
+        for (int S = TWIN - 1; S >= 0; S--) {
+            const int slot = S % FE_PF;
+            if (((S & 7) == 7 || S == TWIN - 1) && (S >> 3) >= 2) chunk[(S >> 3) - 2] = tw[(S >> 3) - 2];
+            const f32x2 m = m_next;
+            if (FAST) {
+                // the next sample's conversion sits in the middle of this sample's FMAs
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int k = r * D + HP - S;
+                    if (k >= 0 && k < NT) acc[r] = fe_fma(ring[slot][r >> 1], r & 1, m, acc[r]);
+                    if (r == R / 2 - 1 && S > 0) m_next = sample(S - 1);
+                }
+            } else {
+                // all products of the sample first, then the adds, in program order (volatile asm):
+                // no add waits on the product issued just before it
+                f32x2 prod[R];
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int k = r * D + HP - S;
+                    if (k >= 0 && k < NT) prod[r] = fe_mul_v(ring[slot][r >> 1], r & 1, m);
+                }
+                if (S > 0) m_next = sample(S - 1);
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int k = r * D + HP - S;
+                    if (k >= 0 && k < NT) acc[r] = fe_add_v(acc[r], prod[r]);
+                }
+            }
+            if (S - FE_PF >= 0) {
+#pragma unroll
+                for (int q = 0; q < R / 2; q++) ring[slot][q] = hsd[(S - FE_PF) * (R / 2) + q];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- discriminator (demod.cpp:8-19); the previous output of lane t's first comes from t-1
+        const f32x2 left = f32x2{__shfl_up(acc[R - 1].x, 1), __shfl_up(acc[R - 1].y, 1)};
+        float* out = fm + (size_t)ch * fm_stride;
+        const int cbase = c0 + t * R;
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const int k = r * D + HP - S;
-            if (k >= 0 && k < NT) {
-                const float hk = tap[r];
-                if (FAST) acc[r] = __builtin_elementwise_fma(f32x2{hk, hk}, m, acc[r]);
-                else acc[r] = acc[r] + f32x2{hk, hk} * m;
+            const int c = cbase + r;
+            f32x2 pv = (r > 0) ? acc[r > 0 ? r - 1 : 0] : left;
+            if (c == 0) {
+                const float2 p = prev_in[ch];
+                pv = f32x2{p.x, p.y};
             }
+            const f32x2 cur = acc[r];
+            float v;
+            if ((cur.x == 0) & (cur.y == 0)) {
+                v = 0.0f;
+            } else {
+                const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
+                const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
+                v = (float)((double)num / den);
+            }
+            if (c > c0 && c >= 0 && c < block_if) out[c] = v;
+            if (c == block_if - 1) prev_out[ch] = make_float2(cur.x, cur.y);
         }
-        if (S - FE_PF >= 0) {
-#pragma unroll
-            for (int q = 0; q < R / 4; q++) ring[slot][q] = tt4[(S - FE_PF) * (R / 4) + q];
+        if (j == 0) {
+            const uint8_t* src = iq + (size_t)ch * iq_stride;
+            const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
+            uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
+            for (int i = t; i < HP; i += NTH) tout[i] = last[i];
+            const float* o = fm_other + (size_t)ch * fm_stride;
+            for (int i = t; i < HIST; i += NTH) out[i - HIST] = o[block_if - HIST + i];
         }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- discriminator (demod.cpp:8-19); the previous output of lane t's first comes from lane t-1
-    const f32x2 left = f32x2{__shfl_up(acc[R - 1].x, 1), __shfl_up(acc[R - 1].y, 1)};
-    float* out = fm + (size_t)ch * fm_stride;
-    const int cbase = c0 + t * R;
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int c = cbase + r;
-        f32x2 pv = (r > 0) ? acc[r > 0 ? r - 1 : 0] : left;
-        if (c == 0) {
-            const float2 p = prev_in[ch];
-            pv = f32x2{p.x, p.y};
-        }
-        const f32x2 cur = acc[r];
-        float v;
-        if ((cur.x == 0) & (cur.y == 0)) {
-            v = 0.0f;
-        } else {
-            const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
-            const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
-            v = (float)((double)num / den);
-        }
-        if (c > c0 && c >= 0 && c < block_if) out[c] = v;
-        if (c == block_if - 1) prev_out[ch] = make_float2(cur.x, cur.y);
-    }
-    if (blockIdx.x == 0) {
-        const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
-        uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
-        for (int i = t; i < HP; i += NTH) tout[i] = last[i];
-        const float* o = fm_other + (size_t)ch * fm_stride;
-        for (int i = t; i < HIST; i += NTH) out[i - HIST] = o[block_if - HIST + i];
+        __syncthreads();                              // LDS is rewritten by the next tile
+        tile = next;
     }
 }
 
@@ -434,6 +538,22 @@ __global__ __launch_bounds__(BLK) void k_resample(const float* __restrict__ xa, 
 // Both write out[0] = lastCarrier and out[i+1] = t_i (the f32 NCO phase); k_nco_out then turns
 // t_i into cos(t_i*ncoScale + phaseAdjust) in parallel (pll.cpp:52) and updates lastCarrier.
 // ------------------------------------------------------------------------------------------
+// One PLL instance over nch channels (pll.cpp:4 arguments). A launch runs up to 2 of them
+// (blockIdx.y), so the stereo (19 kHz) and RDS (114 kHz) PLLs of a block share one dispatch.
+struct PllJob {
+    const float* in;
+    size_t in_stride;
+    float* tbuf;
+    size_t t_stride;
+    float* out;
+    size_t out_stride;
+    sdr_pll_state* st;
+    float freq, Fs, bw, ncoScale, phaseAdjust;
+};
+struct PllJobs {
+    PllJob j[2];
+};
+
 struct PllRegs {
     float fbI, fbQ, integ, ph;
     double toff, c, s, phi;
@@ -513,12 +633,18 @@ constexpr int PLL_CHUNK = 16;
 // chunk's inputs are prefetched with float4 loads one chunk ahead and the 16 phases are stored
 // with float4 stores -- the unrolled chunk itself touches no memory.
 template <bool VEC>
-__global__ __launch_bounds__(64) void k_pll(const float* __restrict__ in, size_t in_stride, int n, int nch,
-                                            float freq, float Fs, float* __restrict__ tbuf, size_t t_stride,
-                                            float* __restrict__ out, size_t out_stride,
-                                            sdr_pll_state* __restrict__ st, float normBandwidth) {
+__global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) {
     const int ch = blockIdx.x * blockDim.x + threadIdx.x;
     if (ch >= nch) return;
+    const PllJob& jb = jobs.j[blockIdx.y];
+    const float* __restrict__ in = jb.in;
+    const size_t in_stride = jb.in_stride, t_stride = jb.t_stride, out_stride = jb.out_stride;
+    float* __restrict__ tbuf = jb.tbuf;
+    float* __restrict__ out = jb.out;
+    sdr_pll_state* __restrict__ st = jb.st;
+    const float freq = jb.freq, Fs = jb.Fs, normBandwidth = jb.bw;
+    // the serial PLL bounds every block-step: let its waves win issue arbitration on shared SIMDs
+    __builtin_amdgcn_s_setprio(3);
     const float Cp = 2.666;
     const float Ci = 3.555;
     const float Kp = normBandwidth * Cp;
@@ -529,39 +655,46 @@ __global__ __launch_bounds__(64) void k_pll(const float* __restrict__ in, size_t
     float* tb = tbuf + (size_t)ch * t_stride;
     out[(size_t)ch * out_stride] = s0.lastCarrier;             // pll.cpp:18
     PllRegs r = pll_load(s0, w);
-    const int nfull = VEC ? (n / PLL_CHUNK) * PLL_CHUNK : 0;
-    float4 xa[PLL_CHUNK / 4];
-    if (nfull > 0) {
+    // chunks of PLL_CHUNK steps run the unchecked fast path; inputs of the next chunk are loaded
+    // while the current one computes (float4 when rows are 16-byte aligned, VEC)
+    const int nfull = (n / PLL_CHUNK) * PLL_CHUNK;
+    float xa[PLL_CHUNK];
+    auto load_chunk = [&](float* dst, int i0) {
+        if (VEC) {
 #pragma unroll
-        for (int k = 0; k < PLL_CHUNK / 4; k++) xa[k] = reinterpret_cast<const float4*>(x)[k];
-    }
-    for (int i0 = 0; i0 < nfull; i0 += PLL_CHUNK) {
-        float4 xn[PLL_CHUNK / 4];
-        const bool more = i0 + PLL_CHUNK < nfull;
-        if (more) {
+            for (int k = 0; k < PLL_CHUNK / 4; k++) {
+                const float4 v = reinterpret_cast<const float4*>(x + i0)[k];
+                dst[4 * k] = v.x; dst[4 * k + 1] = v.y; dst[4 * k + 2] = v.z; dst[4 * k + 3] = v.w;
+            }
+        } else {
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK / 4; k++) xn[k] = reinterpret_cast<const float4*>(x + i0 + PLL_CHUNK)[k];
+            for (int k = 0; k < PLL_CHUNK; k++) dst[k] = x[i0 + k];
         }
+    };
+    if (nfull > 0) load_chunk(xa, 0);
+    for (int i0 = 0; i0 < nfull; i0 += PLL_CHUNK) {
+        float xn[PLL_CHUNK];
+        const bool more = i0 + PLL_CHUNK < nfull;
+        if (more) load_chunk(xn, i0 + PLL_CHUNK);
         const PllRegs snap = r;
         PllProof pf;
         float tv[PLL_CHUNK];
 #pragma unroll
-        for (int j = 0; j < PLL_CHUNK; j++) {
-            const float4 v4 = xa[j >> 2];
-            const float xv = (j & 3) == 0 ? v4.x : (j & 3) == 1 ? v4.y : (j & 3) == 2 ? v4.z : v4.w;
-            pll_step<false>(r, xv, Kp, Ki, w, tv[j], pf);
-        }
+        for (int j = 0; j < PLL_CHUNK; j++) pll_step<false>(r, xa[j], Kp, Ki, w, tv[j], pf);
         if (!pf.ok()) {
             r = snap;
             for (int j = 0; j < PLL_CHUNK; j++) pll_step<true>(r, x[i0 + j], Kp, Ki, w, tb[i0 + j], pf);
-        } else {
+        } else if (VEC) {
 #pragma unroll
             for (int k = 0; k < PLL_CHUNK / 4; k++)
                 reinterpret_cast<float4*>(tb + i0)[k] = make_float4(tv[4 * k], tv[4 * k + 1], tv[4 * k + 2], tv[4 * k + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < PLL_CHUNK; k++) tb[i0 + k] = tv[k];
         }
         if (more) {
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK / 4; k++) xa[k] = xn[k];
+            for (int k = 0; k < PLL_CHUNK; k++) xa[k] = xn[k];
         }
     }
     {
@@ -577,12 +710,16 @@ __global__ __launch_bounds__(64) void k_pll(const float* __restrict__ in, size_t
     st[ch] = s1;                                               // lastCarrier: k_nco_out
 }
 
-__global__ __launch_bounds__(64) void k_pll_libm(const float* __restrict__ in, size_t in_stride, int n, int nch,
-                                                 float freq, float Fs, float* __restrict__ tbuf, size_t t_stride,
-                                                 float* __restrict__ out, size_t out_stride,
-                                                 sdr_pll_state* __restrict__ st, float normBandwidth) {
+__global__ __launch_bounds__(64) void k_pll_libm(const PllJobs jobs, int n, int nch) {
     const int ch = blockIdx.x * blockDim.x + threadIdx.x;
     if (ch >= nch) return;
+    const PllJob& jb = jobs.j[blockIdx.y];
+    const float* __restrict__ in = jb.in;
+    const size_t in_stride = jb.in_stride, t_stride = jb.t_stride, out_stride = jb.out_stride;
+    float* __restrict__ tbuf = jb.tbuf;
+    float* __restrict__ out = jb.out;
+    sdr_pll_state* __restrict__ st = jb.st;
+    const float freq = jb.freq, Fs = jb.Fs, normBandwidth = jb.bw;
     const float Cp = 2.666;
     const float Ci = 3.555;
     const float Kp = normBandwidth * Cp;
@@ -619,12 +756,16 @@ __global__ __launch_bounds__(64) void k_pll_libm(const float* __restrict__ in, s
 
 // out[ch][i+1]: t_i -> (float)cos((double)(t_i*ncoScale + phaseAdjust)) (pll.cpp:52), in parallel;
 // lastCarrier <- out[ch][n] (pll.cpp:58)
-__global__ __launch_bounds__(BLK) void k_nco_out(const float* __restrict__ tbuf, size_t t_stride,
-                                                 float* __restrict__ out, size_t out_stride, int n,
-                                                 sdr_pll_state* __restrict__ st, float ncoScale, float phaseAdjust) {
+__global__ __launch_bounds__(BLK) void k_nco_out(const PllJobs jobs, int n) {
     const int ch = blockIdx.y;
     const int i = blockIdx.x * BLK + threadIdx.x;
     if (i >= n) return;
+    const PllJob& jb = jobs.j[blockIdx.z];
+    const float* __restrict__ tbuf = jb.tbuf;
+    const size_t t_stride = jb.t_stride, out_stride = jb.out_stride;
+    float* __restrict__ out = jb.out;
+    sdr_pll_state* __restrict__ st = jb.st;
+    const float ncoScale = jb.ncoScale, phaseAdjust = jb.phaseAdjust;
     float* o = out + (size_t)ch * out_stride + 1;
     const float t = tbuf[(size_t)ch * t_stride + i];
     const float a = t * ncoScale + phaseAdjust;
@@ -930,29 +1071,35 @@ bool pll_libm_env() {
     return v;
 }
 
-int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
-               size_t t_stride, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale, float phaseAdjust,
-               float bw, hipStream_t s) {
-    const dim3 g(cdiv(nch, 64)), b(64);
-    const bool vec = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (in_stride % 4 == 0) &&
-                     (reinterpret_cast<uintptr_t>(tbuf) % 16 == 0) && (t_stride % 4 == 0);
+int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
+    const dim3 g(cdiv(nch, 64), njobs), b(64);
+    bool vec = true;
+    for (int k = 0; k < njobs; k++) {
+        const PllJob& j = jobs.j[k];
+        vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
+              (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0);
+    }
     if (libm || pll_libm_env()) {
-        hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, in, in_stride, n, nch, freq, Fs, tbuf, t_stride, out, out_stride,
-                           st, bw);
+        hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, jobs, n, nch);
     } else if (vec) {
-        hipLaunchKernelGGL(k_pll<true>, g, b, 0, s, in, in_stride, n, nch, freq, Fs, tbuf, t_stride, out, out_stride,
-                           st, bw);
+        hipLaunchKernelGGL(k_pll<true>, g, b, 0, s, jobs, n, nch);
     } else {
-        hipLaunchKernelGGL(k_pll<false>, g, b, 0, s, in, in_stride, n, nch, freq, Fs, tbuf, t_stride, out,
-                           out_stride, st, bw);
+        hipLaunchKernelGGL(k_pll<false>, g, b, 0, s, jobs, n, nch);
     }
     LAUNCH_CHECK();
     if (n > 0) {
-        hipLaunchKernelGGL(k_nco_out, dim3(cdiv(n, BLK), nch), dim3(BLK), 0, s, tbuf, t_stride, out, out_stride, n, st,
-                           ncoScale, phaseAdjust);
+        hipLaunchKernelGGL(k_nco_out, dim3(cdiv(n, BLK), nch, njobs), dim3(BLK), 0, s, jobs, n);
         LAUNCH_CHECK();
     }
     return SDR_OK;
+}
+
+int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
+               size_t t_stride, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale, float phaseAdjust,
+               float bw, hipStream_t s) {
+    PllJobs jobs{};
+    jobs.j[0] = PllJob{in, in_stride, tbuf, t_stride, out, out_stride, st, freq, Fs, bw, ncoScale, phaseAdjust};
+    return launch_plls(libm, jobs, 1, n, nch, s);
 }
 
 
@@ -979,19 +1126,28 @@ struct sdr_ctx {
     float *pilot = nullptr, *band = nullptr, *gpilot = nullptr, *carrier = nullptr, *ipll = nullptr,
           *rds_clean = nullptr, *t_st = nullptr, *t_rds = nullptr;
     size_t plain_stride = 0, pll_stride = 0, clean_stride = 0;
+    size_t plain_par = 0, pll_par = 0;                  // pilot/band/gpilot and carrier/ipll are
+                                                        // [2 parities][nch][...] so that the stages
+                                                        // split at the PLL can overlap blocks
     // state
     uint8_t* tail = nullptr;                            // [2][nch][2*(ntaps-1)]
     float2* prev = nullptr;                             // [2][nch]
     sdr_pll_state *st_pll = nullptr, *rds_pll = nullptr;
     int32_t* dec = nullptr;                             // [nch][DEC_STATE]
+    int fe_grid = 0;                                    // front-end workgroups (0: one per tile)
+    int fe_r = 8;                                       // front-end outputs per lane (4 or 8)
+    uint32_t* pad80 = nullptr;                          // 64 words of u8 128 (the zero sample)
     int parity = 1;                                     // parity of the current block
     long long block = -1;                               // index of the current block
     long long stereo_done = -1, rds_dsp_done = -1, rds_bits_done = -1, mono_done = -1;
+    long long st_pre_done = -1, st_pll_done = -1, rds_pre_done = -1, rds_pll_done = -1;
     std::vector<void*> allocs;
 
     float* fm_cur() const { return fm + parity * fm_par; }
     float* fm_oth() const { return fm + (parity ^ 1) * fm_par; }
     float* ext(float* base, size_t par, int p) const { return base + p * par; }
+    float* plain(float* base) const { return base + parity * plain_par; }
+    float* pllbuf(float* base) const { return base + parity * pll_par; }
 };
 
 namespace {
@@ -1061,11 +1217,26 @@ int init_state(sdr_ctx* c, hipStream_t s) {
     c->parity = 1;
     c->block = -1;
     c->stereo_done = c->rds_dsp_done = c->rds_bits_done = c->mono_done = -1;
+    c->st_pre_done = c->st_pll_done = c->rds_pre_done = c->rds_pll_done = -1;
     (void)in;
     return SDR_OK;
 }
 
 inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+}  // namespace
+
+namespace {
+PllJob stereo_job(sdr_ctx* c) {   // stereo.cpp:77: fmpll(pilot, 19e3, rf_Fs/rf_decim, ..., 2.0, 0, 0.01)
+    const sdr_info& in = c->info;
+    return PllJob{c->plain(c->pilot), c->plain_stride, c->t_st, c->plain_stride, c->pllbuf(c->carrier), c->pll_stride,
+                  c->st_pll, 19e3f, (float)(in.rf_Fs / in.rf_decim), 0.01f, 2.0f, 0.0f};
+}
+PllJob rds_job(sdr_ctx* c) {      // rds.cpp:119: fmpll(gen_pilot, 114e3, if_Fs, ..., 0.5, 0, 0.001)
+    const sdr_info& in = c->info;
+    return PllJob{c->plain(c->gpilot), c->plain_stride, c->t_rds, c->plain_stride, c->pllbuf(c->ipll), c->pll_stride,
+                  c->rds_pll, 114e3f, (float)in.if_Fs, 0.001f, 0.5f, 0.0f};
+}
 
 }  // namespace
 
@@ -1087,6 +1258,20 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     c->mode = mode;
     c->rds_on = rds_on ? 1 : 0;
     c->flags = flags;
+    {
+        // One tile per workgroup by default: measured as fast as a persistent grid in isolation and
+        // 2.5x faster while the other streams' kernels share the chip (the dispatcher balances).
+        int cus = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (const char* e = std::getenv("SDR_FE_WG_PER_CU")) {   // tuning knob: persistent grid, k per CU
+            const int k = std::atoi(e);
+            if (k >= 0 && cus > 0) c->fe_grid = k * cus;
+        }
+        if (const char* e = std::getenv("SDR_FE_R")) {           // tuning knob: outputs per lane
+            const int k = std::atoi(e);
+            if (k == 4 || k == 8) c->fe_r = k;
+        }
+    }
     int r = fill_info(&c->info, nch, mode, c->rds_on);
     if (r) { delete c; return r; }
     const sdr_info& in = c->info;
@@ -1113,7 +1298,7 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     {
         // front-end v2 tap table: row S (input sample S of a thread window, R = 8 outputs) holds
         // h[r*D + 100 - S] / 128 (exact power-of-two scaling) or 0 where that tap does not exist
-        const int R = 8, D = in.rf_decim, TWIN = (R - 1) * D + T;
+        const int R = c->fe_r, D = in.rf_decim, TWIN = (R - 1) * D + T;
         std::vector<float> tt((size_t)TWIN * R, 0.0f);
         for (int S_ = 0; S_ < TWIN; S_++)
             for (int r = 0; r < R; r++) {
@@ -1145,15 +1330,21 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     c->plain_stride = round_up((size_t)in.block_if, 64);
     c->pll_stride = round_up((size_t)in.block_if + 1, 64);
     c->clean_stride = round_up((size_t)in.n_rds, 64);
-    TRY(dalloc(c, &c->pilot, c->plain_stride * nch));
-    TRY(dalloc(c, &c->band, c->plain_stride * nch));
-    TRY(dalloc(c, &c->gpilot, c->plain_stride * nch));
+    c->plain_par = c->plain_stride * nch;
+    c->pll_par = c->pll_stride * nch;
+    TRY(dalloc(c, &c->pilot, 2 * c->plain_par));
+    TRY(dalloc(c, &c->band, 2 * c->plain_par));
+    TRY(dalloc(c, &c->gpilot, 2 * c->plain_par));
     TRY(dalloc(c, &c->t_st, c->plain_stride * nch));
     TRY(dalloc(c, &c->t_rds, c->plain_stride * nch));
-    TRY(dalloc(c, &c->carrier, c->pll_stride * nch));
-    TRY(dalloc(c, &c->ipll, c->pll_stride * nch));
+    TRY(dalloc(c, &c->carrier, 2 * c->pll_par));
+    TRY(dalloc(c, &c->ipll, 2 * c->pll_par));
     TRY(dalloc(c, &c->rds_clean, c->clean_stride * nch));
     TRY(dalloc(c, &c->tail, (size_t)2 * nch * 2 * (T - 1)));
+    {
+        std::vector<uint32_t> pad(64, 0x80808080u);
+        TRY(upload(c, &c->pad80, pad));
+    }
     TRY(dalloc(c, &c->prev, (size_t)2 * nch));
     TRY(dalloc(c, &c->st_pll, (size_t)nch));
     TRY(dalloc(c, &c->rds_pll, (size_t)nch));
@@ -1198,17 +1389,27 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     const bool fast = (c->flags & SDR_FLAG_FAST_FRONTEND) != 0;
     float* fm_p = c->fm + p * c->fm_par;
     const float* fm_o = c->fm + (p ^ 1) * c->fm_par;
-    constexpr int R = 8;
-    const dim3 g2(cdiv(in.block_if + 1, 64 * R - 1), c->nch);
-#define FE2(DD, FF)                                                                                          \
-    hipLaunchKernelGGL((k_frontend2<R, DD, FF>), g2, dim3(64), 0, S(stream), iq, iq_stride, tail_in, tail_out,   \
-                       prev_in, prev_out, c->rf_hs, in.block_iq, in.block_if, fm_p, fm_o, c->fm_stride)
+    const int R = c->fe_r;
+    const int tiles_ch = cdiv(in.block_if + 1, 64 * R - 1);
+    const int total = tiles_ch * c->nch;
+    // fe_grid == 0: one tile per workgroup (the hardware dispatcher balances the load when other
+    // streams share the chip); otherwise a persistent grid that prefetches its next tile
+    const dim3 g2(c->fe_grid > 0 ? std::min(total, c->fe_grid) : total);
+#define FE2(RR, DD, FF)                                                                                      \
+    hipLaunchKernelGGL((k_frontend2<RR, DD, FF>), g2, dim3(64), 0, S(stream), iq, iq_stride, tail_in, tail_out,  \
+                       prev_in, prev_out, c->rf_hs, in.block_iq, in.block_if, fm_p, fm_o, c->fm_stride, c->nch,   \
+                       tiles_ch, c->pad80)
+#define FE2R(DD)                                                                                             \
+    do {                                                                                                     \
+        if (R == 8) { if (fast) FE2(8, DD, true); else FE2(8, DD, false); }                                  \
+        else { if (fast) FE2(4, DD, true); else FE2(4, DD, false); }                                         \
+    } while (0)
     if (c->ntaps == 101 && in.rf_decim == 10) {
-        if (fast) FE2(10, true); else FE2(10, false);
+        FE2R(10);
     } else if (c->ntaps == 101 && in.rf_decim == 4) {
-        if (fast) FE2(4, true); else FE2(4, false);
+        FE2R(4);
     } else if (c->ntaps == 101 && in.rf_decim == 3) {
-        if (fast) FE2(3, true); else FE2(3, false);
+        FE2R(3);
     } else {
         const int tile = FIR_TILE;
         dim3 grid(cdiv(in.block_if, tile), c->nch);
@@ -1217,6 +1418,7 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
                            prev_out, c->rf_h, c->ntaps, in.rf_decim, in.block_iq, in.block_if, tile, fm_p, fm_o,
                            c->fm_stride);
     }
+#undef FE2R
 #undef FE2
     LAUNCH_CHECK();
     c->parity = p;
@@ -1249,30 +1451,52 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
     return SDR_OK;
 }
 
-int sdr_stereo(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
-    if (!c || !lr) return fail(SDR_E_INVALID, "null argument");
-    if (c->block < 0 || c->stereo_done == c->block) return fail(SDR_E_INVALID, "stereo: no new block");
+// The stereo and RDS loop bodies split at their PLL (pre: FIRs feeding the PLL; pll: the serial
+// recurrence; post: everything after it), so a caller can run the PLL of block b on its own stream
+// back to back with block b+1's while other streams do the rest. Intermediates that cross the
+// split are kept per block parity. sdr_stereo / sdr_rds_dsp run the three parts on one stream.
+int sdr_stereo_pre(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->block < 0 || c->st_pre_done == c->block) return fail(SDR_E_INVALID, "stereo_pre: no new block");
     const sdr_info& in = c->info;
-    hipStream_t s = S(stream);
     const int n = in.block_if, T = c->ntaps;
     const float* fm = c->fm_cur();
     // pilot BPF (stereo.cpp:74) + band BPF (:80) from one staged window of fm_demod
     dim3 gf(cdiv(n, FIR_TILE), c->nch);
-    hipLaunchKernelGGL((k_fir<2, false>), gf, dim3(BLK), fir_lds_bytes(T, 2, FIR_TILE, 1), s, fm, c->fm_stride, fm,
-                       c->fm_stride, c->pilot_h, c->stereo_h, T, 1, n, FIR_TILE, c->pilot, c->band, c->plain_stride);
+    hipLaunchKernelGGL((k_fir<2, false>), gf, dim3(BLK), fir_lds_bytes(T, 2, FIR_TILE, 1), S(stream), fm,
+                       c->fm_stride, fm, c->fm_stride, c->pilot_h, c->stereo_h, T, 1, n, FIR_TILE, c->plain(c->pilot),
+                       c->plain(c->band), c->plain_stride);
     LAUNCH_CHECK();
-    // PLL 19 kHz -> 38 kHz carrier (:77)
-    {
-        const int r = launch_pll(c->flags & SDR_FLAG_PLL_LIBM, c->pilot, c->plain_stride, n, c->nch, 19e3f,
-                                 (float)(in.rf_Fs / in.rf_decim), c->t_st, c->plain_stride, c->carrier, c->pll_stride,
-                                 c->st_pll, 2.0f, 0.0f, 0.01f, s);
-        if (r) return r;
-    }
-    // mixer (:83-85) into the extended stereo_dc stream
+    c->st_pre_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_stereo_pll(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->st_pre_done != c->block || c->st_pll_done == c->block)
+        return fail(SDR_E_INVALID, "stereo_pll: run sdr_stereo_pre on a new block first");
+    PllJobs jobs{};
+    jobs.j[0] = stereo_job(c);   // PLL 19 kHz -> 38 kHz carrier (stereo.cpp:77)
+    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 1, c->info.block_if, c->nch, S(stream));
+    if (r) return r;
+    c->st_pll_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
+    if (!c || !lr) return fail(SDR_E_INVALID, "null argument");
+    if (c->st_pll_done != c->block || c->stereo_done == c->block)
+        return fail(SDR_E_INVALID, "stereo_post: run sdr_stereo_pll on a new block first");
+    const sdr_info& in = c->info;
+    hipStream_t s = S(stream);
+    const int n = in.block_if;
+    const float* fm = c->fm_cur();
+    // mixer (stereo.cpp:83-85) into the extended stereo_dc stream
     const int p = c->parity;
     float* sdc = c->sdc + p * c->fm_par;
-    hipLaunchKernelGGL(k_mix<false>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, c->band, c->plain_stride,
-                       c->carrier, c->pll_stride, n, sdc, c->sdc + (p ^ 1) * c->fm_par, c->fm_stride, 0);
+    hipLaunchKernelGGL(k_mix<false>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, c->plain(c->band),
+                       c->plain_stride, c->pllbuf(c->carrier), c->pll_stride, n, sdc, c->sdc + (p ^ 1) * c->fm_par,
+                       c->fm_stride, 0);
     LAUNCH_CHECK();
     // mono delay (:88, exact 50-sample shift of fm_demod) + both resamplers + L/R (:94-107)
     const int tile = 512;
@@ -1286,16 +1510,23 @@ int sdr_stereo(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
     return SDR_OK;
 }
 
-int sdr_rds_dsp(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
+int sdr_stereo(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
+    if (!c || !lr) return fail(SDR_E_INVALID, "null argument");
+    if (c->block < 0 || c->stereo_done == c->block) return fail(SDR_E_INVALID, "stereo: no new block");
+    int r = sdr_stereo_pre(c, stream);
+    if (!r) r = sdr_stereo_pll(c, stream);
+    if (!r) r = sdr_stereo_post(c, lr, lr_stride, stream);
+    return r;
+}
+
+int sdr_rds_pre(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
-    if (c->block < 0 || c->rds_dsp_done == c->block) return fail(SDR_E_INVALID, "rds: no new block");
+    if (c->block < 0 || c->rds_pre_done == c->block) return fail(SDR_E_INVALID, "rds_pre: no new block");
     const sdr_info& in = c->info;
     hipStream_t s = S(stream);
     const int n = in.block_if, T = c->ntaps, p = c->parity;
     const float* fm = c->fm_cur();
     float* rband = c->rband + p * c->fm_par;
-    float* rdc = c->rdc + p * c->fm_par;
-    float* rfilt = c->rfilt + p * c->rf_par;
     dim3 gf(cdiv(n, FIR_TILE), c->nch);
     // RDS band BPF (rds.cpp:105) into the extended rds_band stream
     hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rband, c->rband + (p ^ 1) * c->fm_par,
@@ -1306,19 +1537,52 @@ int sdr_rds_dsp(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
     LAUNCH_CHECK();
     // squaring (:111-113) + 114 kHz BPF (:116)
     hipLaunchKernelGGL((k_fir<1, true>), gf, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, rband, c->fm_stride,
-                       rband, c->fm_stride, c->rds_sq_h, nullptr, T, 1, n, FIR_TILE, c->gpilot, nullptr,
+                       rband, c->fm_stride, c->rds_sq_h, nullptr, T, 1, n, FIR_TILE, c->plain(c->gpilot), nullptr,
                        c->plain_stride);
     LAUNCH_CHECK();
-    // PLL 114 kHz -> 57 kHz (:119)
-    {
-        const int r = launch_pll(c->flags & SDR_FLAG_PLL_LIBM, c->gpilot, c->plain_stride, n, c->nch, 114e3f,
-                                 (float)in.if_Fs, c->t_rds, c->plain_stride, c->ipll, c->pll_stride, c->rds_pll, 0.5f,
-                                 0.0f, 0.001f, s);
-        if (r) return r;
-    }
-    // delay (:122) + mixer (:125-127) into the extended rds_dc stream
-    hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride, c->ipll,
-                       c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
+    c->rds_pre_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_rds_pll(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->rds_pre_done != c->block || c->rds_pll_done == c->block)
+        return fail(SDR_E_INVALID, "rds_pll: run sdr_rds_pre on a new block first");
+    PllJobs jobs{};
+    jobs.j[0] = rds_job(c);      // PLL 114 kHz -> 57 kHz (rds.cpp:119)
+    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 1, c->info.block_if, c->nch, S(stream));
+    if (r) return r;
+    c->rds_pll_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_plls(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->st_pre_done != c->block || c->st_pll_done == c->block || c->rds_pre_done != c->block ||
+        c->rds_pll_done == c->block)
+        return fail(SDR_E_INVALID, "plls: run sdr_stereo_pre and sdr_rds_pre on a new block first");
+    PllJobs jobs{};
+    jobs.j[0] = stereo_job(c);
+    jobs.j[1] = rds_job(c);
+    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 2, c->info.block_if, c->nch, S(stream));
+    if (r) return r;
+    c->st_pll_done = c->rds_pll_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->rds_pll_done != c->block || c->rds_dsp_done == c->block)
+        return fail(SDR_E_INVALID, "rds_post: run sdr_rds_pll on a new block first");
+    const sdr_info& in = c->info;
+    hipStream_t s = S(stream);
+    const int n = in.block_if, T = c->ntaps, p = c->parity;
+    float* rband = c->rband + p * c->fm_par;
+    float* rdc = c->rdc + p * c->fm_par;
+    float* rfilt = c->rfilt + p * c->rf_par;
+    // delay (rds.cpp:122) + mixer (:125-127) into the extended rds_dc stream
+    hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride,
+                       c->pllbuf(c->ipll), c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
     LAUNCH_CHECK();
     // 247/640 resampler (:130) into the extended rds_filt stream
     hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rfilt, c->rfilt + (p ^ 1) * c->rf_par,
@@ -1345,6 +1609,15 @@ int sdr_rds_dsp(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
     return SDR_OK;
 }
 
+int sdr_rds_dsp(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->block < 0 || c->rds_dsp_done == c->block) return fail(SDR_E_INVALID, "rds: no new block");
+    int r = sdr_rds_pre(c, stream);
+    if (!r) r = sdr_rds_pll(c, stream);
+    if (!r) r = sdr_rds_post(c, rds_clean, rds_stride, stream);
+    return r;
+}
+
 int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, size_t sym_stride, int32_t* nbits,
                  uint8_t* bits, size_t bits_stride, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
@@ -1365,13 +1638,13 @@ int sdr_ctx_buffer(sdr_ctx* c, const char* name, const float** ptr, size_t* stri
     const int p = c->parity;
     struct E { const char* n; const float* p; size_t s; int l; } tab[] = {
         {"fm", c->fm_cur(), c->fm_stride, in.block_if},
-        {"pilot", c->pilot, c->plain_stride, in.block_if},
-        {"carrier", c->carrier, c->pll_stride, in.block_if + 1},
-        {"band", c->band, c->plain_stride, in.block_if},
+        {"pilot", c->plain(c->pilot), c->plain_stride, in.block_if},
+        {"carrier", c->pllbuf(c->carrier), c->pll_stride, in.block_if + 1},
+        {"band", c->plain(c->band), c->plain_stride, in.block_if},
         {"stereo_dc", c->sdc + p * c->fm_par, c->fm_stride, in.block_if},
         {"rds_band", c->rband + p * c->fm_par, c->fm_stride, in.block_if},
-        {"gen_pilot", c->gpilot, c->plain_stride, in.block_if},
-        {"ipll", c->ipll, c->pll_stride, in.block_if + 1},
+        {"gen_pilot", c->plain(c->gpilot), c->plain_stride, in.block_if},
+        {"ipll", c->pllbuf(c->ipll), c->pll_stride, in.block_if + 1},
         {"rds_dc", c->rdc + p * c->fm_par, c->fm_stride, in.block_if},
         {"rds_filt", c->rfilt + p * c->rf_par, c->rf_stride, in.n_rds},
         {"rds_clean", c->rds_clean, c->clean_stride, in.n_rds},

@@ -183,3 +183,66 @@ def test_fast_frontend_tolerance_and_rds_bits(pkg, synth, golden_long, oracle, t
         for b, want in enumerate(golden_long["channels"][str(c)]["blocks"]):
             if "bits" in want:
                 assert _bitstr(out["bits"][b][j], int(out["nbits"][b][j])) == want["bits"], f"bits ch{c} block {b}"
+
+
+@pytest.mark.parametrize("fused_plls", [False, True], ids=["two_pll_streams", "sdr_plls"])
+def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_plls):
+    """bench.py's schedule: the stereo/RDS bodies split at the PLL (sdr_*_pre/_pll/_post, or both
+    PLLs in one sdr_plls dispatch) on separate streams with the PLLs of block b+1 overlapping block
+    b's post part -- identical audio, rds_clean and RDS bits to the one-stream sequential pipeline,
+    block by block."""
+    torch = torch_cuda
+    nch, nb = 40, 14
+    iqs = [channel_input(synth, 300 + c, nb) for c in range(nch)]
+    d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
+    ref = _run_pipeline(pkg, torch, iqs, nb)
+    pipe = pkg.Pipeline(nch)
+    info = pipe.info
+    s_fe, s_pst, s_prd, s_post = (torch.cuda.Stream() for _ in range(4))
+    ev = lambda: torch.cuda.Event()  # noqa: E731
+    pre, pst, prd, post = ([ev() for _ in range(nb)] for _ in range(4))
+    lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device="cuda") for _ in range(2)]
+    mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device="cuda")
+    clean = torch.empty(nch, info.n_rds, dtype=torch.float32, device="cuda")
+    got = {"mono": [], "stereo": [], "clean": [], "bits": [], "nbits": []}
+    for b in range(nb):
+        if b >= 2:
+            s_fe.wait_event(post[b - 2])
+        pipe.frontend(d[b], stream=s_fe)
+        pipe.mono(mono, stream=s_fe)
+        with torch.cuda.stream(s_fe):
+            got["mono"].append(mono.clone())
+        pipe.stereo_pre(stream=s_fe)
+        pipe.rds_pre(stream=s_fe)
+        pre[b].record(s_fe)
+        if fused_plls:
+            s_pst.wait_event(pre[b])
+            pipe.plls(stream=s_pst)
+            pst[b].record(s_pst)
+            prd[b].record(s_pst)
+        else:
+            s_pst.wait_event(pre[b])
+            pipe.stereo_pll(stream=s_pst)
+            pst[b].record(s_pst)
+            s_prd.wait_event(pre[b])
+            pipe.rds_pll(stream=s_prd)
+            prd[b].record(s_prd)
+        s_post.wait_event(pst[b])
+        s_post.wait_event(prd[b])
+        pipe.stereo_post(lr[b % 2], stream=s_post)
+        pipe.rds_post(clean, bits=True, stream=s_post)
+        with torch.cuda.stream(s_post):
+            got["stereo"].append(lr[b % 2].clone())
+            got["clean"].append(clean.clone())
+            got["bits"].append(pipe.bits.clone())
+            got["nbits"].append(pipe.nbits.clone())
+        post[b].record(s_post)
+    torch.cuda.synchronize()
+    for b in range(nb):
+        assert np.array_equal(got["mono"][b].cpu().numpy(), ref["mono"][b]), f"mono block {b}"
+        assert np.array_equal(got["stereo"][b].cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
+        assert np.array_equal(got["clean"][b].cpu().numpy().view(np.uint32), ref["clean"][b].view(np.uint32)), \
+            f"rds_clean block {b}"
+        assert np.array_equal(got["nbits"][b].cpu().numpy(), ref["nbits"][b]), f"nbits block {b}"
+        assert np.array_equal(got["bits"][b].cpu().numpy(), ref["bits"][b]), f"bits block {b}"
+    pipe.close()
