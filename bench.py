@@ -56,7 +56,10 @@ def make_input(torch, nch: int, nblocks: int, first_channel: int, device):
         src = synth.FMMultiplexSource(first_channel + c)
         for b in range(nblocks):
             host[b, c] = src.next_block()
-    d = torch.empty((nblocks, nch, 2 * synth.BLOCK_IQ), dtype=torch.uint8, device=device)
+    # rows padded to a multiple of 16 bytes (147008 for 147000): the front end then stages whole
+    # 16-byte I/Q groups
+    row = 2 * synth.BLOCK_IQ
+    d = torch.empty((nblocks, nch, (row + 15) // 16 * 16), dtype=torch.uint8, device=device)[:, :, :row]
     reps = (nch + distinct - 1) // distinct
     src_t = torch.from_numpy(host).to(device)
     for r in range(reps):

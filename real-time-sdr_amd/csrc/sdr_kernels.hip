@@ -209,6 +209,212 @@ __device__ __forceinline__ f32x2 fe_fma(double hpair, int hi, f32x2 m, f32x2 acc
     return r;
 }
 
+// ------------------------------------------------------------------------------------------
+// Fast-mode front end on the matrix cores (SDR_FLAG_FAST_FRONTEND): the decimating FIR as an
+// integer GEMM. A wave owns a tile of FT_NB blocks of 16 consecutive decimated outputs of one
+// channel. Block b's outputs need a 256-sample window w_b (x[D*c_b - 100 + s], s < 256, of which
+// 15*D + 101 are used) and y[c_b + i] = sum_s W[i][s] * w_b[s] with the Toeplitz tap matrix
+// W[i][s] = h[D*i + 100 - s]. Samples are exact int8 (u8 - 128); the taps are fixed point with
+// 2^-(31 - ceil(log2 max|h|)) resolution split into FT_ND = 4 balanced base-256 digits, so
+// v_mfma_i32_16x16x64_i8 (rows = 16 outputs, columns = 8 blocks x {I, Q}, K = 4 x 64) accumulates
+// each digit plane exactly in int32 and the planes combine exactly in f64: y is the correctly
+// rounded f32 of the convolution with the quantised taps (<= ~1e-8 absolute from the exact one,
+// so ~1e-6 relative even at 1-LSB input amplitude; 3 digits measured 1e-4 on a filter start-up
+// transient). North-star tolerance 1e-5 relative on fm_demod, RDS bits bit-exact: tested.
+// Staging: u8 I/Q pairs -> planar int8 I and Q rows in LDS (v_perm deinterleave); each B
+// fragment is then one ds_read_b128 (16 consecutive samples of one component).
+// ------------------------------------------------------------------------------------------
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int FT_NB = 32;                 // 16-output blocks per wave tile (4 C tiles of 8 blocks)
+constexpr int FT_TO = 16 * FT_NB;         // outputs computed per tile
+// Tile j computes outputs c0 .. c0 + FT_TO - 1 with c0 = j*ADV - CARRY and writes the ADV outputs
+// from c0 + CARRY on (the CARRY >= 1 before them feed the discriminator). (ADV, CARRY) per D make
+// the first staged sample m0 = c0*D - 100 a multiple of 8 (16-byte I/Q groups) on every tile.
+constexpr int ft_adv(int D) { return D == 3 ? 504 : 508; }
+constexpr int ft_carry(int D) { return D == 10 ? 2 : D == 4 ? 1 : 4; }
+constexpr int FT_ND = 4;                  // digit planes (32-bit fixed-point taps)
+constexpr int FT_AFRAGS = 4 * FT_ND;      // K steps x digit planes
+constexpr int ft_win(int D) { return 16 * D * (FT_NB - 1) + 256; }
+// tiles per workgroup: with 2 the second tile's loads overlap the first's MFMAs, but the 44 extra
+// VGPRs drop occupancy to 2 waves/SIMD, measured slower (0.062 vs 0.051 ms at 1024 channels)
+constexpr int FT_TPW = 1;
+constexpr int c0_mod4(int adv, int carry) { return (adv % 4 == 0) ? -carry : 0; }   // c0 = j*adv - carry
+
+template <int D, bool X4, int TPW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_frontend_mfma(
+    const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
+    uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
+    const v4i* __restrict__ afrag, double yscale, int block_iq, int block_if,
+    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int tiles_ch,
+    const uint32_t* __restrict__ pad) {
+    static_assert(15 * D + 101 <= 256, "one block's window must fit K = 256");
+    constexpr int HP = 100, WIN = ft_win(D), G = WIN / 8;
+    constexpr int ADV = ft_adv(D), CARRY = ft_carry(D);
+    static_assert(CARRY >= 1 && CARRY + ADV <= FT_TO && WIN % 8 == 0, "tile geometry");
+    static_assert(((ADV * D) % 8) == 0 && (((-CARRY * D - HP) % 8) + 8) % 8 == 0, "m0 = 0 mod 8");
+    __shared__ __attribute__((aligned(16))) int8_t plane[2][WIN];
+    const int t = threadIdx.x;
+    // a workgroup takes TPW consecutive tiles of one channel; the next tile's window is loaded
+    // into registers while the current one computes out of LDS
+    const int groups_ch = (tiles_ch + TPW - 1) / TPW;
+    const int ch = blockIdx.x / groups_ch;
+    const int j0 = (blockIdx.x - ch * groups_ch) * TPW, jn = min(j0 + TPW, tiles_ch);
+    const uint8_t* src = iq + (size_t)ch * iq_stride;
+    float* out = fm + (size_t)ch * fm_stride;
+    // ---- stage: groups of 8 I/Q pairs (16 bytes) -> 8 I bytes + 8 Q bytes, signed. The taps'
+    // A fragments (constant, L2-resident, lane-major: every load is 1 KiB contiguous) and all of
+    // a lane's window loads are issued before any is used (fully unrolled).
+    constexpr int GPL = (G + 63) / 64;                // groups per lane
+    v4i A[FT_AFRAGS];
+#pragma unroll
+    for (int f = 0; f < FT_AFRAGS; f++) A[f] = afrag[f * 64 + t];
+    uint4 st[GPL];
+    auto load_window = [&](int jj) {
+        const int m0 = (jj * ADV - CARRY) * D - HP;   // = 0 mod 8
+        const uint2* g2 = reinterpret_cast<const uint2*>(src);
+        const uint2* t2 = reinterpret_cast<const uint2*>(tail_in + (size_t)ch * 2 * HP);
+        const uint2* p2 = reinterpret_cast<const uint2*>(pad);
+        const bool interior = (m0 >= 0) && (m0 + WIN <= block_iq);
+        if (interior && X4) {                         // 16-byte aligned rows: one dwordx4 per group
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4* gw = reinterpret_cast<const u32x4*>(src + 2 * m0);
+#pragma unroll
+            for (int k = 0; k < GPL; k++) {
+                const int i = t + 64 * k;
+                const u32x4 v = (k < GPL - 1 || i < G) ? __builtin_nontemporal_load(gw + i) : u32x4{0u, 0u, 0u, 0u};
+                st[k] = uint4{v.x, v.y, v.z, v.w};
+            }
+        } else {                                      // 8-byte loads, each from the block, the tail or padding
+#pragma unroll
+            for (int k = 0; k < GPL; k++) {
+                uint2 h[2];
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    const int mm = m0 + 8 * (t + 64 * k) + 4 * hh;
+                    const uint2* pa = mm >= 0 ? (mm < block_iq ? g2 + (mm >> 2) : p2)
+                                              : (mm >= -HP ? t2 + ((HP + mm) >> 2) : p2);
+                    h[hh] = *pa;
+                }
+                st[k] = uint4{h[0].x, h[0].y, h[1].x, h[1].y};
+            }
+        }
+    };
+    load_window(j0);
+    for (int j = j0; j < jn; j++) {
+        const int c0 = j * ADV - CARRY;
+        {
+            uint2* pi = reinterpret_cast<uint2*>(plane[0]);
+            uint2* pq = reinterpret_cast<uint2*>(plane[1]);
+#pragma unroll
+            for (int k = 0; k < GPL; k++) {
+                const int i = t + 64 * k;
+                if (k < GPL - 1 || i < G) {
+                    const uint4 v = st[k];
+                    pi[i] = uint2{__builtin_amdgcn_perm(v.y, v.x, 0x06040200u) ^ 0x80808080u,
+                                  __builtin_amdgcn_perm(v.w, v.z, 0x06040200u) ^ 0x80808080u};
+                    pq[i] = uint2{__builtin_amdgcn_perm(v.y, v.x, 0x07050301u) ^ 0x80808080u,
+                                  __builtin_amdgcn_perm(v.w, v.z, 0x07050301u) ^ 0x80808080u};
+                }
+            }
+        }
+        __syncthreads();
+        if constexpr (TPW > 1) {
+            if (j + 1 < jn) load_window(j + 1);       // in flight during this tile's MFMAs
+        }
+        const int n = t & 15, g = t >> 4, comp = n & 1;
+        const int8_t* prow = plane[comp];
+        float carry_i = 0.0f, carry_q = 0.0f;             // last output of the previous C tile
+#pragma unroll 1
+        for (int ct = 0; ct < FT_NB / 8; ct++) {
+            const int bb = 8 * ct + (n >> 1);             // this lane's block
+            v4i acc[FT_ND];
+#pragma unroll
+            for (int p = 0; p < FT_ND; p++) acc[p] = v4i{0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const v4i B = *reinterpret_cast<const v4i*>(prow + 16 * D * bb + 64 * kk + 16 * g);
+#pragma unroll
+                for (int p = 0; p < FT_ND; p++)
+                    acc[p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[FT_ND * kk + p], B, acc[p], 0, 0, 0);
+            }
+            // exact recombination of the digit planes (|sum| < 2^53), one rounding to f32
+            static_assert(FT_ND == 4, "pairwise recombination assumes 4 digit planes");
+            float y[4], yo[4], pI, pQ;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                // digits pair up exactly in int32 (|acc| <= 101 * 128 * 128 < 2^21), the pairs in f64
+                const int hi = (acc[0][r] << 8) + acc[1][r], lo = (acc[2][r] << 8) + acc[3][r];
+                y[r] = (float)(((double)hi * 65536.0 + (double)lo) * yscale);
+                // (I, Q) of rows 4g..4g+3 of block bb: I on even lanes, Q on odd lanes (DPP quad_perm 1,0,3,2)
+                yo[r] = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, y[r]), 0xB1, 0xF,
+                                                                           0xF, false));
+            }
+            const float I3 = comp ? yo[3] : y[3], Q3 = comp ? y[3] : yo[3];
+            // previous output of row 4g: row 4g-1 of the same block (lane t-16), or row 15 of block bb-1
+            // (lane t-2+48), or for the first block of the C tile the carry from the previous one
+            const int src_lane = g > 0 ? t - 16 : ((n >> 1) > 0 ? t - 2 + 48 : t);
+            const float sI = __shfl(I3, src_lane), sQ = __shfl(Q3, src_lane);
+            pI = (g == 0 && (n >> 1) == 0) ? carry_i : sI;
+            pQ = (g == 0 && (n >> 1) == 0) ? carry_q : sQ;
+            carry_i = __shfl(I3, 62);
+            carry_q = __shfl(Q3, 62);
+            if (comp == 0) {
+                const int cb = c0 + 16 * bb + 4 * g;      // output index of row 4g
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float cI = y[r], cQ = yo[r];
+                    float qI = r == 0 ? pI : y[r - 1], qQ = r == 0 ? pQ : yo[r - 1];
+                    const int c = cb + r;
+                    if (c == 0) {
+                        const float2 pv = prev_in[ch];
+                        qI = pv.x;
+                        qQ = pv.y;
+                    }
+                    if ((cI == 0) & (cQ == 0)) {
+                        v[r] = 0.0f;
+                    } else {
+                        // demod.cpp:8-19; the quotient from a Newton-refined reciprocal (~2^-50 relative)
+                        // before the f32 rounding: fast mode only
+                        const float num = cI * (cQ - qQ) - cQ * (cI - qI);
+                        const double den = (double)cI * (double)cI + (double)cQ * (double)cQ;
+                        double rc = __builtin_amdgcn_rcp(den);
+                        rc = __builtin_fma(__builtin_fma(-den, rc, 1.0), rc, rc);
+                        rc = __builtin_fma(__builtin_fma(-den, rc, 1.0), rc, rc);
+                        v[r] = (float)((double)num * rc);
+                    }
+                    if (c == block_if - 1) prev_out[ch] = make_float2(cI, cQ);
+                }
+                const int lo = max(c0 + CARRY, 0), hi = min(c0 + CARRY + ADV, block_if);
+                constexpr int AL = (((c0_mod4(ADV, CARRY)) % 4) + 4) % 4;   // cb mod 4 (fm rows are 16-B aligned)
+                if (cb >= lo && cb + 3 < hi) {
+                    if (AL == 0) {
+                        *reinterpret_cast<float4*>(out + cb) = make_float4(v[0], v[1], v[2], v[3]);
+                    } else if (AL == 2) {
+                        *reinterpret_cast<float2*>(out + cb) = make_float2(v[0], v[1]);
+                        *reinterpret_cast<float2*>(out + cb + 2) = make_float2(v[2], v[3]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) out[cb + r] = v[r];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        if (cb + r >= lo && cb + r < hi) out[cb + r] = v[r];
+                }
+            }
+        }
+        if (j == 0) {
+            const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
+            uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
+            for (int i = t; i < HP; i += 64) tout[i] = last[i];
+            const float* o = fm_other + (size_t)ch * fm_stride;
+            for (int i = t; i < HIST; i += 64) out[i - HIST] = o[block_if - HIST + i];
+        }
+        __syncthreads();                              // LDS is rewritten by the next tile
+    }
+}
+
 // Persistent front end: each 64-lane workgroup walks tiles (channel-major, stride gridDim.x).
 // The next tile's u8 window is loaded into registers (coalesced dwords) while the current tile
 // computes out of LDS, then written to LDS -- global latency overlaps the FIR instead of
@@ -1137,6 +1343,9 @@ struct sdr_ctx {
     int fe_grid = 0;                                    // front-end workgroups (0: one per tile)
     int fe_r = 8;                                       // front-end outputs per lane (4 or 8)
     uint32_t* pad80 = nullptr;                          // 64 words of u8 128 (the zero sample)
+    void* fe_afrag = nullptr;                           // MFMA front end: tap digit fragments
+    double fe_yscale = 0.0;                             // 2^-(F+7): fixed-point taps, x = (u-128)/128
+    bool fe_mfma = false;                               // fast mode runs k_frontend_mfma
     int parity = 1;                                     // parity of the current block
     long long block = -1;                               // index of the current block
     long long stereo_done = -1, rds_dsp_done = -1, rds_bits_done = -1, mono_done = -1;
@@ -1307,6 +1516,39 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
             }
         TRY(upload(c, &c->rf_hs, tt));
     }
+    if (T == 101 && (in.rf_decim == 10 || in.rf_decim == 4 || in.rf_decim == 3)) {
+        // MFMA front end: taps as fixed point h*2^F in FT_ND balanced base-256 digits, laid out as
+        // the A fragments of v_mfma_i32_16x16x64_i8: fragment f = FT_ND*kstep + digit, lane l holds
+        // A[row l&15][k = 64*kstep + 16*(l>>4) + jj], A[i][k] = digit(h[D*i + 100 - k])
+        const int D = in.rf_decim;
+        double hmax = 0.0;
+        for (float v : rf) hmax = std::max(hmax, (double)std::fabs(v));
+        const int F = 8 * FT_ND - 2 - (int)std::ceil(std::log2(hmax));   // |h * 2^F| < 2^(8*ND - 2)
+        std::vector<int8_t> dig((size_t)T * FT_ND);
+        for (int k = 0; k < T; k++) {
+            long long q = std::llround((double)rf[k] * std::ldexp(1.0, F));
+            for (int p = FT_ND - 1; p >= 0; p--) {               // least significant digit first
+                int d = (int)(((q % 256) + 256) % 256);
+                if (d >= 128) d -= 256;
+                dig[(size_t)k * FT_ND + p] = (int8_t)d;
+                q = (q - d) / 256;
+            }
+        }
+        std::vector<int8_t> fr((size_t)FT_AFRAGS * 64 * 16, 0);
+        for (int ks = 0; ks < 4; ks++)
+            for (int p = 0; p < FT_ND; p++)
+                for (int l = 0; l < 64; l++)
+                    for (int jj = 0; jj < 16; jj++) {
+                        const int i = l & 15, k = 64 * ks + 16 * (l >> 4) + jj, tap = D * i + 100 - k;
+                        if (tap >= 0 && tap < T)
+                            fr[(((size_t)(FT_ND * ks + p) * 64) + l) * 16 + jj] = dig[(size_t)tap * FT_ND + p];
+                    }
+        int8_t* dfr = nullptr;
+        TRY(upload(c, &dfr, fr));
+        c->fe_afrag = dfr;
+        c->fe_yscale = std::ldexp(1.0, -(F + 7));
+        c->fe_mfma = std::getenv("SDR_FE_FAST_VALU") == nullptr;   // A/B knob: packed-FMA VALU path
+    }
     TRY(upload(c, &c->pilot_h, pilot));
     TRY(upload(c, &c->stereo_h, stereo));
     TRY(upload(c, &c->rds_h, rds));
@@ -1404,7 +1646,23 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
         if (R == 8) { if (fast) FE2(8, DD, true); else FE2(8, DD, false); }                                  \
         else { if (fast) FE2(4, DD, true); else FE2(4, DD, false); }                                         \
     } while (0)
-    if (c->ntaps == 101 && in.rf_decim == 10) {
+    if (fast && c->fe_mfma) {
+        const v4i* af = static_cast<const v4i*>(c->fe_afrag);
+        // 16-byte I/Q group loads need 16-byte aligned rows (e.g. a row stride of 147008 for mode 0)
+        const bool x4 = (iq_stride % 16 == 0) && (reinterpret_cast<uintptr_t>(iq) % 16 == 0);
+#define FEM(DD, XX)                                                                                          \
+    do {                                                                                                     \
+        const int tc = cdiv(in.block_if, ft_adv(DD));                                                        \
+        hipLaunchKernelGGL((k_frontend_mfma<DD, XX, FT_TPW>), dim3(cdiv(tc, FT_TPW) * c->nch), dim3(64), 0,     \
+                           S(stream), iq, iq_stride,                                                         \
+                           tail_in, tail_out, prev_in, prev_out, af, c->fe_yscale, in.block_iq, in.block_if, fm_p, \
+                           fm_o, c->fm_stride, tc, c->pad80);                                                \
+    } while (0)
+        if (in.rf_decim == 10) { if (x4) FEM(10, true); else FEM(10, false); }
+        else if (in.rf_decim == 4) { if (x4) FEM(4, true); else FEM(4, false); }
+        else { if (x4) FEM(3, true); else FEM(3, false); }
+#undef FEM
+    } else if (c->ntaps == 101 && in.rf_decim == 10) {
         FE2R(10);
     } else if (c->ntaps == 101 && in.rf_decim == 4) {
         FE2R(4);

@@ -20,11 +20,16 @@ def torch_cuda():
     return torch
 
 
-def _run_pipeline(pkg, torch, iq_by_ch, nblocks, mode=0, rds_on=True, flags=0):
-    """iq_by_ch: list of [nblocks][2*block_iq] u8 arrays. Returns per-block host outputs."""
+def _run_pipeline(pkg, torch, iq_by_ch, nblocks, mode=0, rds_on=True, flags=0, row_align=1):
+    """iq_by_ch: list of [nblocks][2*block_iq] u8 arrays. Returns per-block host outputs.
+    row_align > 1 pads every channel row to that many bytes (a strided view is passed)."""
     nch = len(iq_by_ch)
     pipe = pkg.Pipeline(nch, mode=mode, rds_on=rds_on, flags=flags)
-    iq = torch.from_numpy(np.stack(iq_by_ch, axis=1)).cuda()  # [blk][ch][bytes]
+    host = np.stack(iq_by_ch, axis=1)  # [blk][ch][bytes]
+    row = host.shape[2]
+    iq = torch.empty(host.shape[0], nch, (row + row_align - 1) // row_align * row_align, dtype=torch.uint8,
+                     device="cuda")[:, :, :row]
+    iq.copy_(torch.from_numpy(host))
     out = {k: [] for k in ("fm", "mono", "stereo", "clean", "offset", "nsym", "symbols", "nbits", "bits")}
     for b in range(nblocks):
         pipe.frontend(iq[b])
@@ -124,6 +129,29 @@ def test_other_modes_vs_oracle(pkg, synth, oracle, torch_cuda, mode):
             assert _bitstr(out["bits"][b][0], int(out["nbits"][b][0])) == _bitstr(ref["bits"][b], len(ref["bits"][b]))
 
 
+@pytest.mark.parametrize("row_align", [1, 16], ids=["rows_8B_aligned", "rows_16B_aligned"])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_fast_frontend_modes_vs_oracle(pkg, synth, oracle, torch_cuda, mode, row_align):
+    """The MFMA front end for every decimation (D = 10, 4, 10, 3): fm_demod within 1e-5 of the
+    reference (normwise per block) on 3 channels x 7 blocks, including the first block (previous
+    block's tail) and the end of each block (padding)."""
+    import real_time_sdr_amd.synth as s
+    ch = oracle.Channel(mode, True)
+    nb, nch = 7, 3
+    iqs = []
+    for c in range(nch):
+        src = s.FMMultiplexSource(40 + c)
+        iqs.append(np.stack([src.next_block(ch.block_iq) for _ in range(nb)]))
+    out = _run_pipeline(pkg, torch_cuda, iqs, nb, mode=mode, flags=pkg.FLAG_FAST_FRONTEND, row_align=row_align)
+    for c in range(nch):
+        ref = oracle.run_channel(iqs[c], mode, True)
+        for b in range(nb):
+            got, want = out["fm"][b][c].astype(np.float64), ref["fm_demod"][b].astype(np.float64)
+            scale = np.max(np.abs(want))
+            err = np.max(np.abs(got - want))
+            assert err <= 1e-5 * scale, f"mode {mode} ch {c} block {b}: {err / scale:.2e}"
+
+
 def test_reset_restarts_stream(pkg, synth, torch_cuda):
     iq = channel_input(synth, 0, 3)
     torch = torch_cuda
@@ -166,14 +194,15 @@ def test_fast_pll_matches_libm_pll(pkg, synth, torch_cuda):
     pb.close()
 
 
-def test_fast_frontend_tolerance_and_rds_bits(pkg, synth, golden_long, oracle, torch_cuda):
-    """SDR_FLAG_FAST_FRONTEND (v_pk_fma_f32 FIR): fm_demod within 1e-5 relative (north-star
-    tolerance; measured ~1e-7) of the reference, and the RDS bit decisions of the 200-block
-    golden run still bit-exact."""
+@pytest.mark.parametrize("row_align", [1, 16], ids=["rows_8B_aligned", "rows_16B_aligned"])
+def test_fast_frontend_tolerance_and_rds_bits(pkg, synth, golden_long, oracle, torch_cuda, row_align):
+    """SDR_FLAG_FAST_FRONTEND (the int8 MFMA front end; 16-byte staging when rows are 16-byte
+    aligned): fm_demod within 1e-5 relative (north-star tolerance) of the reference, and the RDS
+    bit decisions of the 200-block golden run still bit-exact."""
     nb = golden_long["nblocks"]
     chans = [int(c) for c in golden_long["channels"]]
     iqs = [channel_input(synth, c, nb, golden_long["channels"][str(c)]["input_sha256"]) for c in chans]
-    out = _run_pipeline(pkg, torch_cuda, iqs, nb, flags=pkg.FLAG_FAST_FRONTEND)
+    out = _run_pipeline(pkg, torch_cuda, iqs, nb, flags=pkg.FLAG_FAST_FRONTEND, row_align=row_align)
     ref = oracle.run_channel(iqs[0][:8], 0, True)
     for b in range(8):
         got, want = out["fm"][b][0].astype(np.float64), ref["fm_demod"][b].astype(np.float64)
