@@ -10,10 +10,10 @@
 //
 //  * pll_sincos: f32 t -> cos t, sin t. Cody-Waite reduction by pi/2 with a 22/22/53-bit split
 //    (exact first two products for |t| < 2^30), fdlibm's k_sin/k_cos minimax kernels on
-//    |r| <= pi/4 (error < 2^-58), Estrin evaluation. Also returns phi = -t mod 2pi (unwrapped).
+//    |r| <= pi/4 (error < 2^-58), Estrin evaluation. Also returns -t mod 2pi as (q mod 4, -r).
 //  * pll_phase_detect: atan2(eQ, eI) for (eI, eQ) = x*(RN(cos t), -RN(sin t)) (pll.cpp:36-39).
 //    Rotating (eI, eQ) by +t with the f64 cos/sin of the previous step leaves a residual angle
-//    |delta| < 2^-20, so atan2 = phi + pi*[X<0] + Y/X (mod 2pi) with no polynomial at all.
+//    |delta| < 2^-20, so atan2 = -t + pi*[X<0] + Y/X (mod 2pi) with no polynomial at all.
 //
 // Shared by the HIP kernel and the CPU validation (tools/pllmath/validate.cpp): identical code,
 // except the reciprocal seed (device: v_rcp_f64; host: an f32 reciprocal, i.e. a worse seed).
@@ -89,7 +89,8 @@ PLLM_HD uint32_t tie_distance64(double v) {
 
 struct SinCos {
     double c, s;     // cos t, sin t (relative error < 2^-50)
-    double phi;      // -t mod 2pi, in [-7pi/4 - eps, pi/4 + eps] (absolute error < 2^-50)
+    double mr;       // -r, r = t - q*pi/2 in [-pi/4, pi/4] (absolute error < 2^-50)
+    int q3;          // q mod 4: -t = -q3*pi/2 - r (mod 2pi)
     bool ok;         // (float)c and (float)s are RN_f32(cos t), RN_f32(sin t); reduction valid
     uint32_t tie;    // min(tie_distance64(c), tie_distance64(s)): ok needs tie > 128 and |t| < T_MAX
 };
@@ -114,9 +115,14 @@ PLLM_HD SinCos sincos_f32(float t) {
     const double a = swap ? sr : cr;
     const double b = swap ? cr : sr;
     SinCos o;
-    o.c = (((q + 1) & 2) != 0) ? -a : a;     // cos t < 0 in quadrants 1, 2
-    o.s = ((q & 2) != 0) ? -b : b;           // sin t < 0 in quadrants 2, 3
-    o.phi = fma_(-(double)(q & 3), PIO2, -r);
+    // signs as bit flips of the high word: cos t < 0 in quadrants 1, 2 (bit 1 of q + 1), sin t < 0
+    // in quadrants 2, 3 (bit 1 of q)
+    o.c = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, a) ^
+                                         ((uint64_t)(((uint32_t)(q + 1) << 30) & 0x80000000u) << 32));
+    o.s = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, b) ^
+                                         ((uint64_t)(((uint32_t)q << 30) & 0x80000000u) << 32));
+    o.mr = -r;
+    o.q3 = q & 3;
     o.tie = tie_distance64(o.c) < tie_distance64(o.s) ? tie_distance64(o.c) : tie_distance64(o.s);
     o.ok = (__builtin_fabs(x) < T_MAX) && o.tie > 128u;
     return o;
@@ -125,12 +131,14 @@ PLLM_HD SinCos sincos_f32(float t) {
 struct Phase {
     double e;        // atan2(eQ, eI) in [-pi, pi]
     double d;        // residual angle Y/X; the fast path needs |d| < 2^-18 and |e| < pi - 2^-30
+    float ef;        // RN_f32(e + eps): equals RN_f32(e) whenever split == 0
     uint32_t split;  // bits(RN_f32(e - eps)) ^ bits(RN_f32(e + eps)): 0 iff the f32 rounding is safe
-    bool ok;         // (float)e == RN_f32(atan2(eQ, eI))
+    bool ok;         // ef == RN_f32(atan2(eQ, eI))
 };
 
-// atan2(eQ, eI) given c, s, phi = f64 cos t, sin t, -t mod 2pi of the previous step's t.
-PLLM_HD Phase phase_detect(float eI, float eQ, double c, double s, double phi) {
+// atan2(eQ, eI) given c, s = f64 cos t, sin t of the previous step's t and -t mod 2pi as
+// -q3*pi/2 + mr (mr = -r of the reduction): NaN mr (invalid reduction) makes e NaN.
+PLLM_HD Phase phase_detect(float eI, float eQ, double c, double s, double mr, int q3) {
     const double dI = (double)eI, dQ = (double)eQ;
     const double X = fma_(dI, c, -(dQ * s));      // Re((eI + i eQ)(c + i s))
     const double Y = fma_(dI, s, dQ * c);         // Im(...)
@@ -138,12 +146,15 @@ PLLM_HD Phase phase_detect(float eI, float eQ, double c, double s, double phi) {
     const double cc = fma_(-X, r0, 1.0);
     const double qq = Y * r0;
     const double d = fma_(qq, cc, qq);            // Y/X (rel. error ~ seed error^2); NaN/inf if X == 0
-    const double e0 = (phi + (X < 0.0 ? PI : 0.0)) + d;
+    // atan2 = -t + pi*[X < 0] + d = (2*[X < 0] - q3) * pi/2 + (mr + d)   (mod 2pi)
+    const int k = (X < 0.0 ? 2 : 0) - q3;
+    const double e0 = fma_((double)k, PIO2, mr + d);
     const double e = fma_(-__builtin_rint(e0 * (1.0 / TWO_PI)), TWO_PI, e0);   // into [-pi, pi]
     Phase o;
     o.e = e;
     o.d = d;
-    o.split = __builtin_bit_cast(uint32_t, (float)(e - EPS_ABS_E)) ^ __builtin_bit_cast(uint32_t, (float)(e + EPS_ABS_E));
+    o.ef = (float)(e + EPS_ABS_E);
+    o.split = __builtin_bit_cast(uint32_t, (float)(e - EPS_ABS_E)) ^ __builtin_bit_cast(uint32_t, o.ef);
     o.ok = (__builtin_fabs(d) < 0x1p-18) && (__builtin_fabs(e) < PI - 0x1p-30) && o.split == 0u;
     return o;
 }

@@ -762,7 +762,8 @@ struct PllJobs {
 
 struct PllRegs {
     float fbI, fbQ, integ, ph;
-    double toff, c, s, phi;
+    double toff, c, s, mr;   // mr, q3: -t mod 2pi of the previous step's t (pll_math.h)
+    int q3;
 };
 
 __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
@@ -777,7 +778,8 @@ __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
     const pllm::SinCos sc = pllm::sincos_f32(t_prev);
     r.c = sc.c;
     r.s = sc.s;
-    r.phi = (__builtin_fabs((double)t_prev) < pllm::T_MAX) ? sc.phi : __builtin_nan("");
+    r.mr = (__builtin_fabs((double)t_prev) < pllm::T_MAX) ? sc.mr : __builtin_nan("");
+    r.q3 = sc.q3;
     return r;
 }
 
@@ -801,8 +803,8 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, float Kp, float Ki
                                          PllProof& pf) {
     const float eI = x * r.fbI;                               // pll.cpp:36
     const float eQ = x * (-r.fbQ);                            // pll.cpp:37
-    const pllm::Phase p = pllm::phase_detect(eI, eQ, r.c, r.s, r.phi);
-    float e = (float)p.e;
+    const pllm::Phase p = pllm::phase_detect(eI, eQ, r.c, r.s, r.mr, r.q3);
+    float e = p.ef;
     if (CHECKED && !p.ok) e = (float)atan2((double)eQ, (double)eI);  // pll.cpp:39
     r.integ = r.integ + Ki * e;                               // pll.cpp:41
     r.ph = r.ph + Kp * e + r.integ;                           // pll.cpp:42
@@ -811,7 +813,8 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, float Kp, float Ki
     const pllm::SinCos sc = pllm::sincos_f32(t);
     r.c = sc.c;
     r.s = sc.s;
-    r.phi = sc.phi;
+    r.mr = sc.mr;
+    r.q3 = sc.q3;
     r.fbI = (float)sc.c;                                      // pll.cpp:49
     r.fbQ = (float)sc.s;                                      // pll.cpp:50
     if (CHECKED && !sc.ok) {
@@ -821,7 +824,7 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, float Kp, float Ki
         r.fbQ = (float)sv;
         r.c = cv;
         r.s = sv;
-        if (!(__builtin_fabs((double)t) < pllm::T_MAX)) r.phi = __builtin_nan("");
+        if (!(__builtin_fabs((double)t) < pllm::T_MAX)) r.mr = __builtin_nan("");
     }
     if (!CHECKED) {
         pf.dsum = pf.dsum + __builtin_fabs(p.d);

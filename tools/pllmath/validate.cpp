@@ -46,11 +46,11 @@ int main(int argc, char** argv) {
         float x = (float)((U(rng) - 0.5) * std::exp2(-12.0 * U(rng)));
         if (i % 1000 == 0) x = 0.0f;
         const float eI = x * fbI, eQ = x * (-fbQ);
-        const pllm::Phase p = pllm::phase_detect(eI, eQ, r.c, r.s, r.phi);
+        const pllm::Phase p = pllm::phase_detect(eI, eQ, r.c, r.s, r.mr, r.q3);
         if (!p.ok) { pd_bad++; continue; }
         pd_ok++;
         const float ref = (float)std::atan2((double)eQ, (double)eI);
-        if ((float)p.e != ref) {
+        if (p.ef != ref) {
             if (pd_mis < 10) std::printf("atan2 MISMATCH t=%.9g x=%.9g e=%.17g ref=%.9g\n", t, x, p.e, ref);
             pd_mis++;
         }
@@ -66,7 +66,8 @@ int main(int argc, char** argv) {
         const float Kp = bw * Cp, Ki = bw * bw * Ci;
         float fbI = 1, fbQ = 0, integ = 0, ph = 0, rfbI = 1, rfbQ = 0, rinteg = 0, rph = 0;
         double toff = 0, rtoff = 0;
-        double c = 1, s = 0, phi = 0;
+        double c = 1, s = 0, mr = 0;
+        int q3 = 0;
         const long n = N / 8;
         for (long i = 0; i < n; i++) {
             const float xin = (float)(0.1 * std::cos(2 * M_PI * (freq + 3.0 * sig) / Fs * i + sig) +
@@ -85,15 +86,15 @@ int main(int argc, char** argv) {
             // fast
             {
                 const float eI = xin * fbI, eQ = xin * (-fbQ);
-                const pllm::Phase p = pllm::phase_detect(eI, eQ, c, s, phi);
+                const pllm::Phase p = pllm::phase_detect(eI, eQ, c, s, mr, q3);
                 float e;
-                if (p.ok) e = (float)p.e; else { e = (float)std::atan2((double)eQ, (double)eI); fallbacks++; }
+                if (p.ok) e = p.ef; else { e = (float)std::atan2((double)eQ, (double)eI); fallbacks++; }
                 integ = integ + Ki * e;
                 ph = ph + Kp * e + integ;
                 toff += 1.0;
                 const float t = (float)(2 * 3.14159265358979323846 * (freq / Fs) * toff + (double)ph);
                 const pllm::SinCos r = pllm::sincos_f32(t);
-                c = r.c; s = r.s; phi = r.phi;
+                c = r.c; s = r.s; mr = r.mr; q3 = r.q3;
                 if (r.ok) { fbI = (float)r.c; fbQ = (float)r.s; }
                 else { fbI = (float)std::cos((double)t); fbQ = (float)std::sin((double)t); fallbacks++; }
             }
