@@ -755,6 +755,10 @@ struct PllJob {
     size_t out_stride;
     sdr_pll_state* st;
     float freq, Fs, bw, ncoScale, phaseAdjust;
+    // context mode: out[0] (pll.cpp:18) is the previous block's last carrier, read by the NCO from
+    // that block's output row (prev_out[ch][n]); the PLL kernel then never touches lastCarrier, so
+    // the NCO of block b can run on another stream while the PLL of block b+1 runs.
+    const float* prev_out;
 };
 struct PllJobs {
     PllJob j[2];
@@ -862,7 +866,7 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) 
     const sdr_pll_state s0 = st[ch];
     const float* x = in + (size_t)ch * in_stride;
     float* tb = tbuf + (size_t)ch * t_stride;
-    out[(size_t)ch * out_stride] = s0.lastCarrier;             // pll.cpp:18
+    if (!jb.prev_out) out[(size_t)ch * out_stride] = s0.lastCarrier;   // pll.cpp:18
     PllRegs r = pll_load(s0, w);
     // chunks of PLL_CHUNK steps run the unchecked fast path; inputs of the next chunk are loaded
     // while the current one computes (float4 when rows are 16-byte aligned, VEC)
@@ -910,13 +914,12 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) 
         PllProof pf;
         for (int i = nfull; i < n; i++) pll_step<true>(r, x[i], Kp, Ki, w, tb[i], pf);
     }
-    sdr_pll_state s1 = s0;
-    s1.feedbackI = r.fbI;
-    s1.feedbackQ = r.fbQ;
-    s1.integrator = r.integ;
-    s1.phaseEst = r.ph;
-    s1.trigOffset = r.toff;
-    st[ch] = s1;                                               // lastCarrier: k_nco_out
+    // every field but lastCarrier (k_nco_out's)
+    st[ch].feedbackI = r.fbI;
+    st[ch].feedbackQ = r.fbQ;
+    st[ch].integrator = r.integ;
+    st[ch].phaseEst = r.ph;
+    st[ch].trigOffset = r.toff;
 }
 
 __global__ __launch_bounds__(64) void k_pll_libm(const PllJobs jobs, int n, int nch) {
@@ -936,7 +939,7 @@ __global__ __launch_bounds__(64) void k_pll_libm(const PllJobs jobs, int n, int 
     const double w = 2 * 3.14159265358979323846 * (freq / Fs);  // 2*PI*(freq/Fs), pll.cpp:47
     sdr_pll_state s = st[ch];
     const float* x = in + (size_t)ch * in_stride;
-    out[(size_t)ch * out_stride] = s.lastCarrier;
+    if (!jb.prev_out) out[(size_t)ch * out_stride] = s.lastCarrier;
     float* o = tbuf + (size_t)ch * t_stride;
     float fbI = s.feedbackI, fbQ = s.feedbackQ, integ = s.integrator, ph = s.phaseEst;
     double toff = s.trigOffset;
@@ -957,10 +960,11 @@ __global__ __launch_bounds__(64) void k_pll_libm(const PllJobs jobs, int n, int 
     }
     s.feedbackI = fbI;
     s.feedbackQ = fbQ;
-    s.integrator = integ;
-    s.phaseEst = ph;
-    s.trigOffset = toff;
-    st[ch] = s;
+    st[ch].feedbackI = fbI;
+    st[ch].feedbackQ = fbQ;
+    st[ch].integrator = integ;
+    st[ch].phaseEst = ph;
+    st[ch].trigOffset = toff;
 }
 
 // out[ch][i+1]: t_i -> (float)cos((double)(t_i*ncoScale + phaseAdjust)) (pll.cpp:52), in parallel;
@@ -983,6 +987,7 @@ __global__ __launch_bounds__(BLK) void k_nco_out(const PllJobs jobs, int n) {
     if (!sc.ok) v = (float)cos((double)a);
     o[i] = v;
     if (i == n - 1) st[ch].lastCarrier = v;
+    if (i == 0 && jb.prev_out) o[-1] = jb.prev_out[(size_t)ch * out_stride + n];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1223,6 +1228,12 @@ __global__ void k_differential(uint8_t* __restrict__ out, size_t out_stride, con
     last_bit[ch] = b[nb - 1];
 }
 
+// x[ch][col] = v for every channel row (the carried last NCO sample at initialisation)
+__global__ void k_set_col(float* x, size_t stride, int col, int nch, float v) {
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch < nch) x[(size_t)ch * stride + col] = v;
+}
+
 __global__ void k_fill_u8(uint8_t* p, uint8_t v, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -1280,7 +1291,15 @@ bool pll_libm_env() {
     return v;
 }
 
-int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
+int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
+    if (n > 0) {
+        hipLaunchKernelGGL(k_nco_out, dim3(cdiv(n, BLK), nch, njobs), dim3(BLK), 0, s, jobs, n);
+        LAUNCH_CHECK();
+    }
+    return SDR_OK;
+}
+
+int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s, bool with_nco = true) {
     const dim3 g(cdiv(nch, 64), njobs), b(64);
     bool vec = true;
     for (int k = 0; k < njobs; k++) {
@@ -1296,18 +1315,14 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
         hipLaunchKernelGGL(k_pll<false>, g, b, 0, s, jobs, n, nch);
     }
     LAUNCH_CHECK();
-    if (n > 0) {
-        hipLaunchKernelGGL(k_nco_out, dim3(cdiv(n, BLK), nch, njobs), dim3(BLK), 0, s, jobs, n);
-        LAUNCH_CHECK();
-    }
-    return SDR_OK;
+    return with_nco ? launch_nco(jobs, njobs, n, nch, s) : SDR_OK;
 }
 
 int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
                size_t t_stride, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale, float phaseAdjust,
                float bw, hipStream_t s) {
     PllJobs jobs{};
-    jobs.j[0] = PllJob{in, in_stride, tbuf, t_stride, out, out_stride, st, freq, Fs, bw, ncoScale, phaseAdjust};
+    jobs.j[0] = PllJob{in, in_stride, tbuf, t_stride, out, out_stride, st, freq, Fs, bw, ncoScale, phaseAdjust, nullptr};
     return launch_plls(libm, jobs, 1, n, nch, s);
 }
 
@@ -1425,6 +1440,15 @@ int init_state(sdr_ctx* c, hipStream_t s) {
     HIP_TRY(hipMemcpyAsync(c->st_pll, st.data(), st.size() * sizeof(sdr_pll_state), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->rds_pll, st.data(), st.size() * sizeof(sdr_pll_state), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(c->dec, 0, (size_t)c->nch * DEC_STATE * sizeof(int32_t), s));
+    // carrier[0] of the first block = lastCarrier = 1 (stereo.cpp:45): the NCO reads it from the
+    // other parity's row end
+    for (int p = 0; p < 2; p++) {
+        hipLaunchKernelGGL(k_set_col, dim3(cdiv(c->nch, 64)), dim3(64), 0, s, c->carrier + p * c->pll_par, c->pll_stride,
+                           in.block_if, c->nch, 1.0f);
+        hipLaunchKernelGGL(k_set_col, dim3(cdiv(c->nch, 64)), dim3(64), 0, s, c->ipll + p * c->pll_par, c->pll_stride,
+                           in.block_if, c->nch, 1.0f);
+    }
+    LAUNCH_CHECK();
     HIP_TRY(hipStreamSynchronize(s));
     c->parity = 1;
     c->block = -1;
@@ -1441,13 +1465,15 @@ inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 namespace {
 PllJob stereo_job(sdr_ctx* c) {   // stereo.cpp:77: fmpll(pilot, 19e3, rf_Fs/rf_decim, ..., 2.0, 0, 0.01)
     const sdr_info& in = c->info;
-    return PllJob{c->plain(c->pilot), c->plain_stride, c->t_st, c->plain_stride, c->pllbuf(c->carrier), c->pll_stride,
-                  c->st_pll, 19e3f, (float)(in.rf_Fs / in.rf_decim), 0.01f, 2.0f, 0.0f};
+    return PllJob{c->plain(c->pilot), c->plain_stride, c->plain(c->t_st), c->plain_stride, c->pllbuf(c->carrier),
+                  c->pll_stride, c->st_pll, 19e3f, (float)(in.rf_Fs / in.rf_decim), 0.01f, 2.0f, 0.0f,
+                  c->carrier + (c->parity ^ 1) * c->pll_par};
 }
 PllJob rds_job(sdr_ctx* c) {      // rds.cpp:119: fmpll(gen_pilot, 114e3, if_Fs, ..., 0.5, 0, 0.001)
     const sdr_info& in = c->info;
-    return PllJob{c->plain(c->gpilot), c->plain_stride, c->t_rds, c->plain_stride, c->pllbuf(c->ipll), c->pll_stride,
-                  c->rds_pll, 114e3f, (float)in.if_Fs, 0.001f, 0.5f, 0.0f};
+    return PllJob{c->plain(c->gpilot), c->plain_stride, c->plain(c->t_rds), c->plain_stride, c->pllbuf(c->ipll),
+                  c->pll_stride, c->rds_pll, 114e3f, (float)in.if_Fs, 0.001f, 0.5f, 0.0f,
+                  c->ipll + (c->parity ^ 1) * c->pll_par};
 }
 
 }  // namespace
@@ -1580,8 +1606,8 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     TRY(dalloc(c, &c->pilot, 2 * c->plain_par));
     TRY(dalloc(c, &c->band, 2 * c->plain_par));
     TRY(dalloc(c, &c->gpilot, 2 * c->plain_par));
-    TRY(dalloc(c, &c->t_st, c->plain_stride * nch));
-    TRY(dalloc(c, &c->t_rds, c->plain_stride * nch));
+    TRY(dalloc(c, &c->t_st, 2 * c->plain_par));
+    TRY(dalloc(c, &c->t_rds, 2 * c->plain_par));
     TRY(dalloc(c, &c->carrier, 2 * c->pll_par));
     TRY(dalloc(c, &c->ipll, 2 * c->pll_par));
     TRY(dalloc(c, &c->rds_clean, c->clean_stride * nch));
@@ -1737,8 +1763,8 @@ int sdr_stereo_pll(sdr_ctx* c, void* stream) {
     if (c->st_pre_done != c->block || c->st_pll_done == c->block)
         return fail(SDR_E_INVALID, "stereo_pll: run sdr_stereo_pre on a new block first");
     PllJobs jobs{};
-    jobs.j[0] = stereo_job(c);   // PLL 19 kHz -> 38 kHz carrier (stereo.cpp:77)
-    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 1, c->info.block_if, c->nch, S(stream));
+    jobs.j[0] = stereo_job(c);   // PLL 19 kHz -> 38 kHz carrier (stereo.cpp:77); NCO output: stereo_post
+    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 1, c->info.block_if, c->nch, S(stream), false);
     if (r) return r;
     c->st_pll_done = c->block;
     return SDR_OK;
@@ -1752,6 +1778,13 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
     hipStream_t s = S(stream);
     const int n = in.block_if;
     const float* fm = c->fm_cur();
+    {
+        // NCO output of this block's PLL phases (pll.cpp:52), carrier[0] = last of the previous block
+        PllJobs jobs{};
+        jobs.j[0] = stereo_job(c);
+        const int r = launch_nco(jobs, 1, n, c->nch, s);
+        if (r) return r;
+    }
     // mixer (stereo.cpp:83-85) into the extended stereo_dc stream
     const int p = c->parity;
     float* sdc = c->sdc + p * c->fm_par;
@@ -1810,8 +1843,8 @@ int sdr_rds_pll(sdr_ctx* c, void* stream) {
     if (c->rds_pre_done != c->block || c->rds_pll_done == c->block)
         return fail(SDR_E_INVALID, "rds_pll: run sdr_rds_pre on a new block first");
     PllJobs jobs{};
-    jobs.j[0] = rds_job(c);      // PLL 114 kHz -> 57 kHz (rds.cpp:119)
-    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 1, c->info.block_if, c->nch, S(stream));
+    jobs.j[0] = rds_job(c);      // PLL 114 kHz -> 57 kHz (rds.cpp:119); NCO output: rds_post
+    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 1, c->info.block_if, c->nch, S(stream), false);
     if (r) return r;
     c->rds_pll_done = c->block;
     return SDR_OK;
@@ -1825,7 +1858,7 @@ int sdr_plls(sdr_ctx* c, void* stream) {
     PllJobs jobs{};
     jobs.j[0] = stereo_job(c);
     jobs.j[1] = rds_job(c);
-    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 2, c->info.block_if, c->nch, S(stream));
+    const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 2, c->info.block_if, c->nch, S(stream), false);
     if (r) return r;
     c->st_pll_done = c->rds_pll_done = c->block;
     return SDR_OK;
@@ -1841,6 +1874,12 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
     float* rband = c->rband + p * c->fm_par;
     float* rdc = c->rdc + p * c->fm_par;
     float* rfilt = c->rfilt + p * c->rf_par;
+    {
+        PllJobs jobs{};
+        jobs.j[0] = rds_job(c);                       // NCO output of this block's PLL (rds.cpp:119)
+        const int r = launch_nco(jobs, 1, n, c->nch, s);
+        if (r) return r;
+    }
     // delay (rds.cpp:122) + mixer (:125-127) into the extended rds_dc stream
     hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride,
                        c->pllbuf(c->ipll), c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
