@@ -79,7 +79,7 @@ def cpu_baseline(seconds_target: float = 8.0) -> dict | None:
     blob = b"".join(src.next_block().tobytes() for _ in range(nblk_distinct))
     samples_per_blob = nblk_distinct * synth.BLOCK_IQ
     if exe.exists():
-        reps = 60   # 1920 blocks = 141 M I/Q samples (~7 s at the reference's ~20 MS/s)
+        reps = 150  # 4800 blocks = 353 M I/Q samples (~10 s at the reference's ~37 MS/s)
         with tempfile.TemporaryFile() as out:
             t0 = time.perf_counter()
             p = subprocess.Popen([str(exe), "0", "r"], stdin=subprocess.PIPE, stdout=out, stderr=subprocess.DEVNULL)
@@ -135,6 +135,10 @@ def main() -> None:
     ap.add_argument("--channels", type=int, default=1024, help="channels per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL gather (N>1)")
+    ap.add_argument("--no-isolated", action="store_true", help="skip the isolated front-end timings")
+    ap.add_argument("--numerics", choices=("exact", "fast"), default="exact",
+                    help="exact: every output bit-identical to the reference; fast: the matrix-core front end "
+                         "(fm_demod within 1e-5, RDS bits bit-exact)")
     args = ap.parse_args()
 
     import torch
@@ -155,7 +159,8 @@ def main() -> None:
     from real_time_sdr_amd.sharding import channel_range
     first, nch = channel_range(nch, rank)
     iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
-    pipe = pkg.Pipeline(nch, mode=0, rds_on=True, device=local)
+    fast = args.numerics == "fast"
+    pipe = pkg.Pipeline(nch, mode=0, rds_on=True, device=local, flags=pkg.FLAG_FAST_FRONTEND if fast else 0)
     info = pipe.info
     # Three streams, one HIP hardware queue each (GPU_MAX_HW_QUEUES is 4 and one serves the null
     # stream; a fourth stream would share a queue and serialise behind it): front end + mono + the
@@ -232,14 +237,38 @@ def main() -> None:
     total_samples = world * nch * info.block_iq * args.steps
     value = total_samples / elapsed / 1e6
 
+    # informational, outside the timed region: the front-end kernel of both numerics modes alone
+    # on the GPU (one stream, the same resident inputs), for comparison with the in-pipeline figure
+    isolated = {}
+    if rank == 0 and not args.no_isolated:
+        for name, flags in (("exact", 0), ("fast", pkg.FLAG_FAST_FRONTEND)):
+            p2 = pkg.Pipeline(nch, mode=0, rds_on=True, device=local, flags=flags)
+            s2 = torch.cuda.Stream(dev)
+            for b in range(min(nblocks, 3)):
+                p2.frontend(iq[b], stream=s2)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 20
+            e0.record(s2)
+            for b in range(reps):
+                p2.frontend(iq[b % nblocks], stream=s2)
+            e1.record(s2)
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / reps
+            gbs = fe_bytes / (ms / 1e3) / 1e9
+            isolated[name] = {"avg_launch_ms": round(ms, 4), "achieved_GBps": round(gbs, 1),
+                              "frac": round(gbs / HBM_PEAK_GBS, 4)}
+            p2.close()
+
     if rank == 0:
-        prof = ROOT / "profiles" / "pmc_frontend_r01.json"
+        # HBM bytes per launch of the same kernel from rocprofv3 PMC passes (FETCH_SIZE x2 gfx950
+        # correction + WRITE_SIZE; tools/pmc_summary.py), committed under profiles/
+        prof = ROOT / "profiles" / "pmc_frontend.json"
         traffic = None
         if prof.exists():
             try:
                 pm = json.loads(prof.read_text())
                 if pm.get("channels") == nch:
-                    traffic = pm.get("hbm_bytes_per_launch")
+                    traffic = pm.get(args.numerics, {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         res = {
@@ -259,15 +288,19 @@ def main() -> None:
                 "workload": "BASELINE configs[4] per GPU: full mono+stereo+RDS pipeline (project 0 r + mono), "
                             f"{nch} channels/GPU, mode 0 (2.4 MS/s, 73500 I/Q per block)",
                 "channels_per_gpu": nch, "channels_total": world * nch, "block_iq": info.block_iq,
-                "mode": 0, "numerics": "exact (bit-exact with the reference)",
+                "mode": 0,
+                "numerics": ("fast: int8 MFMA front end, fm_demod within 1e-5 of the reference, RDS bits bit-exact"
+                             if fast else "exact (bit-exact with the reference)"),
                 "parallelism": f"channel-sharded x{world}" + ("" if world == 1 or args.no_gather else " + RCCL all-gather"),
             },
             "roofline": {
-                "kernel": "k_frontend (u8 I/Q -> 101-tap FIR /10 on I,Q -> FM discriminator)",
+                "kernel": ("k_frontend_mfma" if fast else "k_frontend2") +
+                          " (u8 I/Q -> 101-tap FIR /10 on I,Q -> FM discriminator)",
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4),
             },
+            "frontend_isolated": isolated or None,
             "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline(),
         }
         print(json.dumps(res))

@@ -9,8 +9,9 @@
 // path (OCML), exactly as the reference computes it.
 //
 //  * pll_sincos: f32 t -> cos t, sin t. Cody-Waite reduction by pi/2 with a 22/22/53-bit split
-//    (exact first two products for |t| < 2^30), fdlibm's k_sin/k_cos minimax kernels on
-//    |r| <= pi/4 (error < 2^-58), Estrin evaluation. Also returns -t mod 2pi as (q mod 4, -r).
+//    (exact first two products for |t| < 2^30), fdlibm's k_sin kernel and a refitted degree-8
+//    cos kernel on |r| <= pi/4 (relative error < 2^-51), Estrin evaluation. Also returns
+//    -t mod 2pi as (q mod 4, -r).
 //  * pll_phase_detect: atan2(eQ, eI) for (eI, eQ) = x*(RN(cos t), -RN(sin t)) (pll.cpp:36-39).
 //    Rotating (eI, eQ) by +t with the f64 cos/sin of the previous step leaves a residual angle
 //    |delta| < 2^-20, so atan2 = -t + pi*[X<0] + Y/X (mod 2pi) with no polynomial at all.
@@ -42,9 +43,10 @@ constexpr double PIO2 = 1.5707963267948966;
 constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
                  S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
                  S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+// cos kernel: degree-4 Q (one coefficient fewer than fdlibm), refitted near-minimax for the
+// relative error of cos on |r| <= pi/4 by tools/pllmath/fit_poly.py: 2^-51.7 in double evaluation
+constexpr double C1 = 0.04166666666659653, C2 = -0.0013888888877611482, C3 = 2.4801580707202765e-05,
+                 C4 = -2.755552309095219e-07, C5 = 2.0645117778725974e-09;
 // error bounds used by the rounding test (generous: measured errors are far smaller)
 constexpr double EPS_ABS_E = 0x1p-45;      // absolute, phase detector output (|e| <= pi)
 constexpr double T_MAX = 0x1p30;           // reduction valid below this
@@ -107,8 +109,8 @@ PLLM_HD SinCos sincos_f32(float t) {
     // sin r = r + r^3 (S1 + z S2 + z^2 (S3 + z S4) + z^4 (S5 + z S6))   (Estrin)
     const double sp = fma_(z4, fma_(z, S6, S5), fma_(z2, fma_(z, S4, S3), fma_(z, S2, S1)));
     const double sr = fma_(r * z, sp, r);
-    // cos r = (1 - z/2) + z^2 (C1 + z C2 + z^2 (C3 + z C4) + z^4 (C5 + z C6))
-    const double cp = fma_(z4, fma_(z, C6, C5), fma_(z2, fma_(z, C4, C3), fma_(z, C2, C1)));
+    // cos r = (1 - z/2) + z^2 (C1 + z C2 + z^2 (C3 + z C4) + z^4 C5)
+    const double cp = fma_(z4, C5, fma_(z2, fma_(z, C4, C3), fma_(z, C2, C1)));
     const double cr = fma_(z2, cp, fma_(z, -0.5, 1.0));
     const int q = (int)kd;                   // |kd| < 2^30 when the reduction is valid
     const bool swap = (q & 1) != 0;

@@ -21,7 +21,7 @@ fi
 if [ "${PROF:-1}" = 1 ]; then
   step rocprof kernel-trace
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
-      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1; rc=$?
+      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-isolated ${BENCH_ARGS:-} > $O/prof.log 2>&1; rc=$?
   [ $rc -eq 0 ] || { tail -20 $O/prof.log; exit $rc; }
   find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
   head -12 $O/kernel_stats.csv | cut -c1-160
@@ -34,6 +34,6 @@ if [ "${PMC:-1}" = 1 ]; then
     [ $rc -eq 0 ] || { tail -20 $O/pmc_$c.log; exit $rc; }
     find $O/pmc_$c -name "*counter_collection.csv" -exec cp {} $O/pmc_$c.csv \;
   done
-  timeout -k 10 60 python tools/pmc_summary.py $O > $O/pmc_summary.json; cat $O/pmc_summary.json
+  timeout -k 10 60 python tools/pmc_summary.py $O 1024 > $O/pmc_summary.json; cat $O/pmc_summary.json
 fi
 step done

@@ -30,19 +30,30 @@ def load(path: pathlib.Path, counter: str) -> dict:
     return per
 
 
+def kernel_name(name: str) -> str:
+    # "void (anonymous namespace)::k_frontend2<8, 10, false>(...)" -> "k_frontend2<8, 10, false>"
+    return name.split("::", 1)[-1].split("(", 1)[0]
+
+
+def mode_of(name: str) -> str:
+    return "fast" if "frontend_mfma" in name or "true>" in name.split("(")[0] else "exact"
+
+
 def main() -> None:
     d = pathlib.Path(sys.argv[1])
     fetch = load(d / "pmc_FETCH_SIZE.csv", "FETCH_SIZE")
     write = load(d / "pmc_WRITE_SIZE.csv", "WRITE_SIZE")
-    out = {}
+    out = {"channels": int(sys.argv[2]) if len(sys.argv) > 2 else 1024,
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over tools/bench_frontend.py; "
+                     "FETCH_SIZE x2 (gfx950 wide-load correction, MI355X_MICROARCH.md HBM section)"}
     for name in sorted(set(fetch) | set(write)):
         f = fetch.get(name, [])
         w = write.get(name, [])
         fb = 2 * 1024 * sum(f) / len(f) if f else None          # KiB -> B, x2 gfx950 correction
         wb = 1024 * sum(w) / len(w) if w else None
-        out[name.split("(")[0]] = {"dispatches": max(len(f), len(w)), "fetch_bytes_corrected": fb,
-                                   "write_bytes": wb,
-                                   "hbm_bytes_per_launch": (fb or 0) + (wb or 0) if fb is not None else None}
+        out[mode_of(name)] = {"kernel": kernel_name(name), "dispatches": max(len(f), len(w)),
+                              "fetch_bytes_corrected": fb, "write_bytes": wb,
+                              "hbm_bytes_per_launch": (fb or 0) + (wb or 0) if fb is not None else None}
     print(json.dumps(out, indent=1))
 
 
