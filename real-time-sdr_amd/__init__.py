@@ -21,7 +21,7 @@ import os
 import pathlib
 
 HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = HERE / "libsdr_amd.so"
+LIB_PATH = pathlib.Path(os.environ["SDR_AMD_LIB"]) if os.environ.get("SDR_AMD_LIB") else HERE / "libsdr_amd.so"  # override: A/B experiments (tools/)
 
 SDR_OK = 0
 SDR_MAX_SYMS = 256

@@ -211,7 +211,7 @@ __device__ __forceinline__ f32x2 fe_fma(double hpair, int hi, f32x2 m, f32x2 acc
 
 // ------------------------------------------------------------------------------------------
 // Fast-mode front end on the matrix cores (SDR_FLAG_FAST_FRONTEND): the decimating FIR as an
-// integer GEMM. A wave owns a tile of FT_NB blocks of 16 consecutive decimated outputs of one
+// integer GEMM. A wave owns a tile of NB (16, 24 or 32; default 32) blocks of 16 consecutive decimated outputs of one
 // channel. Block b's outputs need a 256-sample window w_b (x[D*c_b - 100 + s], s < 256, of which
 // 15*D + 101 are used) and y[c_b + i] = sum_s W[i][s] * w_b[s] with the Toeplitz tap matrix
 // W[i][s] = h[D*i + 100 - s]. Samples are exact int8 (u8 - 128); the taps are fixed point with
@@ -225,22 +225,138 @@ __device__ __forceinline__ f32x2 fe_fma(double hpair, int hi, f32x2 m, f32x2 acc
 // fragment is then one ds_read_b128 (16 consecutive samples of one component).
 // ------------------------------------------------------------------------------------------
 typedef int v4i __attribute__((ext_vector_type(4)));
-constexpr int FT_NB = 32;                 // 16-output blocks per wave tile (4 C tiles of 8 blocks)
-constexpr int FT_TO = 16 * FT_NB;         // outputs computed per tile
-// Tile j computes outputs c0 .. c0 + FT_TO - 1 with c0 = j*ADV - CARRY and writes the ADV outputs
-// from c0 + CARRY on (the CARRY >= 1 before them feed the discriminator). (ADV, CARRY) per D make
-// the first staged sample m0 = c0*D - 100 a multiple of 8 (16-byte I/Q groups) on every tile.
-constexpr int ft_adv(int D) { return D == 3 ? 504 : 508; }
+// NB = 16-output blocks per wave tile (NB/8 C tiles of 8 blocks). Tile j computes outputs
+// c0 .. c0 + 16*NB - 1 with c0 = j*ADV - CARRY and writes the ADV outputs from c0 + CARRY on (the
+// CARRY >= 1 before them feed the discriminator). (ADV, CARRY) per D make the first staged sample
+// m0 = c0*D - 100 a multiple of 8 (16-byte I/Q groups) on every tile.
+constexpr int ft_adv(int D, int NB) { return D == 3 ? 16 * NB - 8 : 16 * NB - 4; }
 constexpr int ft_carry(int D) { return D == 10 ? 2 : D == 4 ? 1 : 4; }
 constexpr int FT_ND = 4;                  // digit planes (32-bit fixed-point taps)
 constexpr int FT_AFRAGS = 4 * FT_ND;      // K steps x digit planes
-constexpr int ft_win(int D) { return 16 * D * (FT_NB - 1) + 256; }
-// tiles per workgroup: with 2 the second tile's loads overlap the first's MFMAs, but the 44 extra
-// VGPRs drop occupancy to 2 waves/SIMD, measured slower (0.062 vs 0.051 ms at 1024 channels)
-constexpr int FT_TPW = 1;
-constexpr int c0_mod4(int adv, int carry) { return (adv % 4 == 0) ? -carry : 0; }   // c0 = j*adv - carry
+constexpr int ft_win(int D, int NB) { return 16 * D * (NB - 1) + 256; }
+constexpr int FT_NB_DEFAULT = 32;
+#ifndef FT_RECOMB_F64
+#define FT_RECOMB_F64 0
+#endif
+#ifndef FT_CT_UNROLL
+#define FT_CT_UNROLL 1
+#endif
 
-template <int D, bool X4, int TPW>
+// One wave tile of the MFMA front end: NB blocks of 16 outputs (c0 + 16*bb + row) from the staged
+// window in LDS, written to out[lo, hi). Shared by the one-tile-per-workgroup kernel (planar image)
+// and the persistent LDS-DMA kernel (raw image).
+template <int D, int NB, bool RAW>
+__device__ __forceinline__ void ft_tile(const int8_t* __restrict__ lds, const v4i (&A)[FT_AFRAGS], double yscale,
+                                        int c0, int ch, const float2* __restrict__ prev_in,
+                                        float2* __restrict__ prev_out, int block_if, float* __restrict__ out) {
+    constexpr int WIN = ft_win(D, NB), ADV = ft_adv(D, NB), CARRY = ft_carry(D);
+    const float ys = (float)yscale;                   // 2^-(F+7): exact in f32
+    const int t = threadIdx.x;
+    // C layout of v_mfma_i32_16x16x64_i8: lane t holds rows 4g..4g+3 (g = t>>4) of column n = t&15;
+    // column n = block 8*ct + (n>>1), component n&1 (I even, Q odd)
+    const int n = t & 15, g = t >> 4, comp = n & 1;
+    // B operand: 16 consecutive samples of this lane's component. Planar image (RAW false): one
+    // 16-byte read of the signed I or Q plane. Raw image (RAW true: the interleaved u8 I/Q bytes as
+    // the LDS-DMA lands them): two 16-byte reads, de-interleaved by v_perm and made signed (u8 ^ 0x80).
+    const int8_t* prow = RAW ? lds : lds + comp * WIN;
+    const uint32_t psel = comp ? 0x07050301u : 0x06040200u;
+    const int lo = max(c0 + CARRY, 0), hi = min(c0 + CARRY + ADV, block_if);
+    float carry_i = 0.0f, carry_q = 0.0f;             // last output of the previous C tile
+#pragma unroll FT_CT_UNROLL
+    for (int ct = 0; ct < NB / 8; ct++) {
+        const int bb = 8 * ct + (n >> 1);             // this lane's block
+        v4i acc[FT_ND];
+#pragma unroll
+        for (int p = 0; p < FT_ND; p++) acc[p] = v4i{0, 0, 0, 0};
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+            v4i B;
+            if (RAW) {
+                const uint4* rp = reinterpret_cast<const uint4*>(prow + 2 * (16 * D * bb + 64 * kk + 16 * g));
+                const uint4 r0 = rp[0], r1 = rp[1];
+                B = v4i{(int)(__builtin_amdgcn_perm(r0.y, r0.x, psel) ^ 0x80808080u),
+                        (int)(__builtin_amdgcn_perm(r0.w, r0.z, psel) ^ 0x80808080u),
+                        (int)(__builtin_amdgcn_perm(r1.y, r1.x, psel) ^ 0x80808080u),
+                        (int)(__builtin_amdgcn_perm(r1.w, r1.z, psel) ^ 0x80808080u)};
+            } else {
+                B = *reinterpret_cast<const v4i*>(prow + 16 * D * bb + 64 * kk + 16 * g);
+            }
+#pragma unroll
+            for (int p = 0; p < FT_ND; p++)
+                acc[p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[FT_ND * kk + p], B, acc[p], 0, 0, 0);
+        }
+        // recombination of the digit planes: y = this lane's component of rows 4g..4g+3, yo = the
+        // other component (DPP quad_perm 1,0,3,2)
+        static_assert(FT_ND == 4, "pairwise recombination assumes 4 digit planes");
+        float y[4], yo[4];
+#if FT_RECOMB_F64
+        (void)ys;
+#endif
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            // digits pair up exactly in int32 (|acc| <= 101 * 128 * 128 < 2^21)
+            const int hi2 = (acc[0][r] << 8) + acc[1][r], lo2 = (acc[2][r] << 8) + acc[3][r];
+#if FT_RECOMB_F64
+            // exact in f64 (|sum| < 2^53), one rounding to f32
+            y[r] = (float)(((double)hi2 * 65536.0 + (double)lo2) * yscale);
+#else
+            // f32: hi2 rounds once (< 2^-24 relative), the power-of-two scalings are exact, one fma:
+            // within ~1 ulp of the exact sum at a quarter of the f64 issue cost
+            y[r] = __builtin_fmaf((float)hi2, ys * 65536.0f, (float)lo2 * ys);
+#endif
+            yo[r] = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, y[r]), 0xB1, 0xF,
+                                                                       0xF, false));
+        }
+        const float I3 = comp ? yo[3] : y[3], Q3 = comp ? y[3] : yo[3];
+        // previous output of row 4g: row 4g-1 of the same block (lane t-16), or row 15 of block bb-1
+        // (lane t-2+48), or for the first block of the C tile the carry from the previous one
+        const int src_lane = g > 0 ? t - 16 : ((n >> 1) > 0 ? t - 2 + 48 : t);
+        const float sI = __shfl(I3, src_lane), sQ = __shfl(Q3, src_lane);
+        const bool first = (g == 0 && (n >> 1) == 0);
+        const float pI = first ? carry_i : sI, pQ = first ? carry_q : sQ;
+        carry_i = __shfl(I3, 62);
+        carry_q = __shfl(Q3, 62);
+        // the discriminator is split over the lane pair: the I lane takes rows 0, 1, the Q lane rows 2, 3
+        const int cb = c0 + 16 * bb + 4 * g + 2 * comp;   // output index of this lane's first row
+        float aI[3], aQ[3];                               // prev, row, row+1
+        {
+            const float I0 = comp ? yo[0] : y[0], Q0 = comp ? y[0] : yo[0];
+            const float I1 = comp ? yo[1] : y[1], Q1 = comp ? y[1] : yo[1];
+            const float I2 = comp ? yo[2] : y[2], Q2 = comp ? y[2] : yo[2];
+            aI[0] = comp ? I1 : pI; aQ[0] = comp ? Q1 : pQ;
+            aI[1] = comp ? I2 : I0; aQ[1] = comp ? Q2 : Q0;
+            aI[2] = comp ? I3 : I1; aQ[2] = comp ? Q3 : Q1;
+        }
+        float v[2];
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const int c = cb + r;
+            float qI = aI[r], qQ = aQ[r];
+            if (c == 0) {
+                const float2 pv = prev_in[ch];
+                qI = pv.x;
+                qQ = pv.y;
+            }
+            const float cI = aI[r + 1], cQ = aQ[r + 1];
+            // demod.cpp:8-19 (numerator as the reference; fast mode only: f32 denominator and a
+            // v_rcp_f32 quotient, a few f32 ulps from the reference's f64 division)
+            const float num = cI * (cQ - qQ) - cQ * (cI - qI);
+            const float den = cI * cI + cQ * cQ;
+            const float q = num * __builtin_amdgcn_rcpf(den);
+            v[r] = ((cI == 0.0f) & (cQ == 0.0f)) ? 0.0f : q;
+            if (c == block_if - 1) prev_out[ch] = make_float2(cI, cQ);
+        }
+        if (cb >= lo && cb + 1 < hi && ((cb & 1) == 0)) {
+            *reinterpret_cast<float2*>(out + cb) = make_float2(v[0], v[1]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 2; r++)
+                if (cb + r >= lo && cb + r < hi) out[cb + r] = v[r];
+        }
+    }
+}
+
+template <int D, bool X4, int NB>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_frontend_mfma(
     const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
     uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
@@ -248,29 +364,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int tiles_ch,
     const uint32_t* __restrict__ pad) {
     static_assert(15 * D + 101 <= 256, "one block's window must fit K = 256");
-    constexpr int HP = 100, WIN = ft_win(D), G = WIN / 8;
-    constexpr int ADV = ft_adv(D), CARRY = ft_carry(D);
-    static_assert(CARRY >= 1 && CARRY + ADV <= FT_TO && WIN % 8 == 0, "tile geometry");
+    static_assert(NB % 8 == 0, "whole C tiles");
+    constexpr int HP = 100, WIN = ft_win(D, NB), G = WIN / 8;
+    constexpr int ADV = ft_adv(D, NB), CARRY = ft_carry(D);
+    static_assert(CARRY >= 1 && CARRY + ADV <= 16 * NB && WIN % 8 == 0, "tile geometry");
     static_assert(((ADV * D) % 8) == 0 && (((-CARRY * D - HP) % 8) + 8) % 8 == 0, "m0 = 0 mod 8");
     __shared__ __attribute__((aligned(16))) int8_t plane[2][WIN];
     const int t = threadIdx.x;
-    // a workgroup takes TPW consecutive tiles of one channel; the next tile's window is loaded
-    // into registers while the current one computes out of LDS
-    const int groups_ch = (tiles_ch + TPW - 1) / TPW;
-    const int ch = blockIdx.x / groups_ch;
-    const int j0 = (blockIdx.x - ch * groups_ch) * TPW, jn = min(j0 + TPW, tiles_ch);
+    const int ch = blockIdx.x / tiles_ch;
+    const int j = blockIdx.x - ch * tiles_ch;
     const uint8_t* src = iq + (size_t)ch * iq_stride;
     float* out = fm + (size_t)ch * fm_stride;
-    // ---- stage: groups of 8 I/Q pairs (16 bytes) -> 8 I bytes + 8 Q bytes, signed. The taps'
-    // A fragments (constant, L2-resident, lane-major: every load is 1 KiB contiguous) and all of
-    // a lane's window loads are issued before any is used (fully unrolled).
+    const int c0 = j * ADV - CARRY;
+    // ---- stage: groups of 8 I/Q pairs (16 bytes) -> 8 I bytes + 8 Q bytes, signed. All of a
+    // lane's window loads are issued first (fully unrolled), then the taps' A fragments (constant,
+    // L2-resident, lane-major: every load is 1 KiB contiguous).
     constexpr int GPL = (G + 63) / 64;                // groups per lane
     v4i A[FT_AFRAGS];
-#pragma unroll
-    for (int f = 0; f < FT_AFRAGS; f++) A[f] = afrag[f * 64 + t];
-    uint4 st[GPL];
-    auto load_window = [&](int jj) {
-        const int m0 = (jj * ADV - CARRY) * D - HP;   // = 0 mod 8
+    {
+        uint4 st[GPL];
+        const int m0 = c0 * D - HP;                   // = 0 mod 8
         const uint2* g2 = reinterpret_cast<const uint2*>(src);
         const uint2* t2 = reinterpret_cast<const uint2*>(tail_in + (size_t)ch * 2 * HP);
         const uint2* p2 = reinterpret_cast<const uint2*>(pad);
@@ -298,120 +411,117 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                 st[k] = uint4{h[0].x, h[0].y, h[1].x, h[1].y};
             }
         }
+        // taps after the window: in flight together, the window (older) is waited for first
+#pragma unroll
+        for (int f = 0; f < FT_AFRAGS; f++) A[f] = afrag[f * 64 + t];
+        uint2* pi = reinterpret_cast<uint2*>(plane[0]);
+        uint2* pq = reinterpret_cast<uint2*>(plane[1]);
+#pragma unroll
+        for (int k = 0; k < GPL; k++) {
+            const int i = t + 64 * k;
+            if (k < GPL - 1 || i < G) {
+                const uint4 v = st[k];
+                pi[i] = uint2{__builtin_amdgcn_perm(v.y, v.x, 0x06040200u) ^ 0x80808080u,
+                              __builtin_amdgcn_perm(v.w, v.z, 0x06040200u) ^ 0x80808080u};
+                pq[i] = uint2{__builtin_amdgcn_perm(v.y, v.x, 0x07050301u) ^ 0x80808080u,
+                              __builtin_amdgcn_perm(v.w, v.z, 0x07050301u) ^ 0x80808080u};
+            }
+        }
+    }
+    __syncthreads();
+    ft_tile<D, NB, false>(plane[0], A, yscale, c0, ch, prev_in, prev_out, block_if, out);
+    if (j == 0) {
+        const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
+        uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
+        for (int i = t; i < HP; i += 64) tout[i] = last[i];
+        const float* o = fm_other + (size_t)ch * fm_stride;
+        for (int i = t; i < HIST; i += 64) out[i - HIST] = o[block_if - HIST + i];
+    }
+}
+
+// Persistent MFMA front end for 16-byte aligned rows: a grid of a few waves per CU (one wave per
+// workgroup) walks tiles round-robin (tile = blockIdx.x + i*gridDim.x; a device-wide atomic queue
+// saturates near 90 dequeues/us, far below the ~500 tiles/us needed), loads the taps' A fragments
+// once, and keeps the NEXT tile's window in flight while it computes the current one: interior windows
+// go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPRs) into the other of two LDS buffers,
+// retired by a counted vmcnt; boundary tiles (the first of a channel reads the previous block's tail,
+// the last runs into the padding) are staged synchronously with plain loads. The B fragments are
+// read from the raw interleaved image (ft_tile<RAW>).
+template <int D, int NB>
+__global__ __launch_bounds__(64) void k_frontend_mfma_q(
+    const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
+    uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
+    const v4i* __restrict__ afrag, double yscale, int block_iq, int block_if,
+    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int tiles_ch, int total,
+    const uint32_t* __restrict__ pad) {
+    constexpr int HP = 100, WIN = ft_win(D, NB), RAWB = 2 * WIN;
+    constexpr int ADV = ft_adv(D, NB), CARRY = ft_carry(D);
+    constexpr int NGL = (RAWB + 1023) / 1024;          // LDS-DMA instructions per window (1 KiB each)
+    constexpr int BUFB = NGL * 1024;
+    static_assert(NGL <= 63, "vmcnt immediate (6 bits)");
+    __shared__ __attribute__((aligned(16))) int8_t lds[2 * BUFB];
+    const int t = threadIdx.x;
+    v4i A[FT_AFRAGS];
+#pragma unroll
+    for (int f = 0; f < FT_AFRAGS; f++) A[f] = afrag[f * 64 + t];
+    // window of tile tl starts at sample m0 = c0*D - 100 (= 0 mod 8); the DMA reads BUFB bytes
+    auto m0_of = [&](int tl) { const int j = tl % tiles_ch; return (j * ADV - CARRY) * D - HP; };
+    auto interior = [&](int tl) { const int m0 = m0_of(tl); return m0 >= 0 && 2 * m0 + BUFB <= 2 * block_iq; };
+    auto issue = [&](int tl, int buf) {
+        const uint8_t* g = iq + (size_t)(tl / tiles_ch) * iq_stride + 2 * (size_t)m0_of(tl) + 16 * t;
+#pragma unroll
+        for (int i = 0; i < NGL; i++)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + 1024 * i),
+                                             reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                                 reinterpret_cast<uintptr_t>(lds + buf * BUFB + 1024 * i)),
+                                             16, 0, 0);
     };
-    load_window(j0);
-    for (int j = j0; j < jn; j++) {
-        const int c0 = j * ADV - CARRY;
-        {
-            uint2* pi = reinterpret_cast<uint2*>(plane[0]);
-            uint2* pq = reinterpret_cast<uint2*>(plane[1]);
-#pragma unroll
-            for (int k = 0; k < GPL; k++) {
-                const int i = t + 64 * k;
-                if (k < GPL - 1 || i < G) {
-                    const uint4 v = st[k];
-                    pi[i] = uint2{__builtin_amdgcn_perm(v.y, v.x, 0x06040200u) ^ 0x80808080u,
-                                  __builtin_amdgcn_perm(v.w, v.z, 0x06040200u) ^ 0x80808080u};
-                    pq[i] = uint2{__builtin_amdgcn_perm(v.y, v.x, 0x07050301u) ^ 0x80808080u,
-                                  __builtin_amdgcn_perm(v.w, v.z, 0x07050301u) ^ 0x80808080u};
-                }
-            }
+    // boundary window: every 8-byte group (4 I/Q pairs) from the block, the previous block's tail or
+    // the padding (u8 128 == 0.0f), plain loads -> ds_write
+    auto stage_plain = [&](int tl, int buf) {
+        const int ch = tl / tiles_ch, m0 = m0_of(tl);
+        const uint2* g2 = reinterpret_cast<const uint2*>(iq + (size_t)ch * iq_stride);
+        const uint2* t2 = reinterpret_cast<const uint2*>(tail_in + (size_t)ch * 2 * HP);
+        const uint2* p2 = reinterpret_cast<const uint2*>(pad);
+        uint2* d = reinterpret_cast<uint2*>(lds + buf * BUFB);
+        for (int i = t; i < RAWB / 8; i += 64) {
+            const int mm = m0 + 4 * i;
+            const uint2* pa = mm >= 0 ? (mm < block_iq ? g2 + (mm >> 2) : p2) : (mm >= -HP ? t2 + ((HP + mm) >> 2) : p2);
+            d[i] = *pa;
         }
-        __syncthreads();
-        if constexpr (TPW > 1) {
-            if (j + 1 < jn) load_window(j + 1);       // in flight during this tile's MFMAs
-        }
-        const int n = t & 15, g = t >> 4, comp = n & 1;
-        const int8_t* prow = plane[comp];
-        float carry_i = 0.0f, carry_q = 0.0f;             // last output of the previous C tile
-#pragma unroll 1
-        for (int ct = 0; ct < FT_NB / 8; ct++) {
-            const int bb = 8 * ct + (n >> 1);             // this lane's block
-            v4i acc[FT_ND];
-#pragma unroll
-            for (int p = 0; p < FT_ND; p++) acc[p] = v4i{0, 0, 0, 0};
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) {
-                const v4i B = *reinterpret_cast<const v4i*>(prow + 16 * D * bb + 64 * kk + 16 * g);
-#pragma unroll
-                for (int p = 0; p < FT_ND; p++)
-                    acc[p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[FT_ND * kk + p], B, acc[p], 0, 0, 0);
-            }
-            // exact recombination of the digit planes (|sum| < 2^53), one rounding to f32
-            static_assert(FT_ND == 4, "pairwise recombination assumes 4 digit planes");
-            float y[4], yo[4], pI, pQ;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                // digits pair up exactly in int32 (|acc| <= 101 * 128 * 128 < 2^21), the pairs in f64
-                const int hi = (acc[0][r] << 8) + acc[1][r], lo = (acc[2][r] << 8) + acc[3][r];
-                y[r] = (float)(((double)hi * 65536.0 + (double)lo) * yscale);
-                // (I, Q) of rows 4g..4g+3 of block bb: I on even lanes, Q on odd lanes (DPP quad_perm 1,0,3,2)
-                yo[r] = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, y[r]), 0xB1, 0xF,
-                                                                           0xF, false));
-            }
-            const float I3 = comp ? yo[3] : y[3], Q3 = comp ? y[3] : yo[3];
-            // previous output of row 4g: row 4g-1 of the same block (lane t-16), or row 15 of block bb-1
-            // (lane t-2+48), or for the first block of the C tile the carry from the previous one
-            const int src_lane = g > 0 ? t - 16 : ((n >> 1) > 0 ? t - 2 + 48 : t);
-            const float sI = __shfl(I3, src_lane), sQ = __shfl(Q3, src_lane);
-            pI = (g == 0 && (n >> 1) == 0) ? carry_i : sI;
-            pQ = (g == 0 && (n >> 1) == 0) ? carry_q : sQ;
-            carry_i = __shfl(I3, 62);
-            carry_q = __shfl(Q3, 62);
-            if (comp == 0) {
-                const int cb = c0 + 16 * bb + 4 * g;      // output index of row 4g
-                float v[4];
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const float cI = y[r], cQ = yo[r];
-                    float qI = r == 0 ? pI : y[r - 1], qQ = r == 0 ? pQ : yo[r - 1];
-                    const int c = cb + r;
-                    if (c == 0) {
-                        const float2 pv = prev_in[ch];
-                        qI = pv.x;
-                        qQ = pv.y;
-                    }
-                    if ((cI == 0) & (cQ == 0)) {
-                        v[r] = 0.0f;
-                    } else {
-                        // demod.cpp:8-19; the quotient from a Newton-refined reciprocal (~2^-50 relative)
-                        // before the f32 rounding: fast mode only
-                        const float num = cI * (cQ - qQ) - cQ * (cI - qI);
-                        const double den = (double)cI * (double)cI + (double)cQ * (double)cQ;
-                        double rc = __builtin_amdgcn_rcp(den);
-                        rc = __builtin_fma(__builtin_fma(-den, rc, 1.0), rc, rc);
-                        rc = __builtin_fma(__builtin_fma(-den, rc, 1.0), rc, rc);
-                        v[r] = (float)((double)num * rc);
-                    }
-                    if (c == block_if - 1) prev_out[ch] = make_float2(cI, cQ);
-                }
-                const int lo = max(c0 + CARRY, 0), hi = min(c0 + CARRY + ADV, block_if);
-                constexpr int AL = (((c0_mod4(ADV, CARRY)) % 4) + 4) % 4;   // cb mod 4 (fm rows are 16-B aligned)
-                if (cb >= lo && cb + 3 < hi) {
-                    if (AL == 0) {
-                        *reinterpret_cast<float4*>(out + cb) = make_float4(v[0], v[1], v[2], v[3]);
-                    } else if (AL == 2) {
-                        *reinterpret_cast<float2*>(out + cb) = make_float2(v[0], v[1]);
-                        *reinterpret_cast<float2*>(out + cb + 2) = make_float2(v[2], v[3]);
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 4; r++) out[cb + r] = v[r];
-                    }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                        if (cb + r >= lo && cb + r < hi) out[cb + r] = v[r];
-                }
-            }
-        }
+    };
+    const int G = gridDim.x;
+    int cur = blockIdx.x, nxt = cur + G;
+    if (cur < total) {
+        if (interior(cur)) issue(cur, 0);
+        else stage_plain(cur, 0);
+    }
+    int b = 0;
+    while (cur < total) {
+        const bool dma_next = nxt < total && interior(nxt);
+        if (dma_next) issue(nxt, b ^ 1);
+        // retire cur's window (everything but the NGL younger DMA of nxt; vector memory operations
+        // retire in issue order, the previous tile's fm stores included) and the boundary ds_writes
+        if (dma_next) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(NGL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const int ch = cur / tiles_ch, j = cur - ch * tiles_ch;
+        float* out = fm + (size_t)ch * fm_stride;
+        ft_tile<D, NB, true>(lds + b * BUFB, A, yscale, j * ADV - CARRY, ch, prev_in, prev_out, block_if, out);
         if (j == 0) {
+            const uint8_t* src = iq + (size_t)ch * iq_stride;
             const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
             uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
             for (int i = t; i < HP; i += 64) tout[i] = last[i];
             const float* o = fm_other + (size_t)ch * fm_stride;
             for (int i = t; i < HIST; i += 64) out[i - HIST] = o[block_if - HIST + i];
         }
-        __syncthreads();                              // LDS is rewritten by the next tile
+        // the other buffer is free: every wave passed this tile's barrier after finishing the previous
+        // tile (one wave per workgroup, so the barrier only orders this wave's own LDS traffic)
+        if (nxt < total && !dma_next) stage_plain(nxt, b ^ 1);
+        cur = nxt;
+        nxt += G;
+        b ^= 1;
     }
 }
 
@@ -1364,6 +1474,7 @@ struct sdr_ctx {
     void* fe_afrag = nullptr;                           // MFMA front end: tap digit fragments
     double fe_yscale = 0.0;                             // 2^-(F+7): fixed-point taps, x = (u-128)/128
     bool fe_mfma = false;                               // fast mode runs k_frontend_mfma
+    int fe_nb = FT_NB_DEFAULT;                          // MFMA front end: 16-output blocks per tile
     int parity = 1;                                     // parity of the current block
     long long block = -1;                               // index of the current block
     long long stereo_done = -1, rds_dsp_done = -1, rds_bits_done = -1, mono_done = -1;
@@ -1577,6 +1688,7 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
         c->fe_afrag = dfr;
         c->fe_yscale = std::ldexp(1.0, -(F + 7));
         c->fe_mfma = std::getenv("SDR_FE_FAST_VALU") == nullptr;   // A/B knob: packed-FMA VALU path
+        if (const char* e = std::getenv("SDR_FE_NB")) c->fe_nb = std::atoi(e);   // tuning knob: 16, 24, 32
     }
     TRY(upload(c, &c->pilot_h, pilot));
     TRY(upload(c, &c->stereo_h, stereo));
@@ -1679,17 +1791,28 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
         const v4i* af = static_cast<const v4i*>(c->fe_afrag);
         // 16-byte I/Q group loads need 16-byte aligned rows (e.g. a row stride of 147008 for mode 0)
         const bool x4 = (iq_stride % 16 == 0) && (reinterpret_cast<uintptr_t>(iq) % 16 == 0);
-#define FEM(DD, XX)                                                                                          \
+#define FEM(DD, XX, NB)                                                                                      \
     do {                                                                                                     \
-        const int tc = cdiv(in.block_if, ft_adv(DD));                                                        \
-        hipLaunchKernelGGL((k_frontend_mfma<DD, XX, FT_TPW>), dim3(cdiv(tc, FT_TPW) * c->nch), dim3(64), 0,     \
-                           S(stream), iq, iq_stride,                                                         \
-                           tail_in, tail_out, prev_in, prev_out, af, c->fe_yscale, in.block_iq, in.block_if, fm_p, \
-                           fm_o, c->fm_stride, tc, c->pad80);                                                \
+        const int tc = cdiv(in.block_if, ft_adv(DD, NB));                                                    \
+        if (XX && c->fe_grid > 0) {                                                                          \
+            hipLaunchKernelGGL((k_frontend_mfma_q<DD, NB>), dim3(std::min(tc * c->nch, c->fe_grid)), dim3(64), \
+                               0, S(stream), iq, iq_stride, tail_in, tail_out, prev_in, prev_out, af,        \
+                               c->fe_yscale, in.block_iq, in.block_if, fm_p, fm_o, c->fm_stride, tc,          \
+                               tc * c->nch, c->pad80);                                                       \
+        } else {                                                                                             \
+            hipLaunchKernelGGL((k_frontend_mfma<DD, XX, NB>), dim3(tc * c->nch), dim3(64), 0,                \
+                               S(stream), iq, iq_stride,                                                     \
+                               tail_in, tail_out, prev_in, prev_out, af, c->fe_yscale, in.block_iq, in.block_if, \
+                               fm_p, fm_o, c->fm_stride, tc, c->pad80);                                      \
+        }                                                                                                    \
     } while (0)
-        if (in.rf_decim == 10) { if (x4) FEM(10, true); else FEM(10, false); }
-        else if (in.rf_decim == 4) { if (x4) FEM(4, true); else FEM(4, false); }
-        else { if (x4) FEM(3, true); else FEM(3, false); }
+#define FEMN(DD, XX) do { if (c->fe_nb == 16) FEM(DD, XX, 16); else if (c->fe_nb == 24) FEM(DD, XX, 24); \
+                             else if (c->fe_nb == 48) FEM(DD, XX, 48); else if (c->fe_nb == 64) FEM(DD, XX, 64); \
+                             else FEM(DD, XX, 32); } while (0)
+        if (in.rf_decim == 10) { if (x4) FEMN(10, true); else FEMN(10, false); }
+        else if (in.rf_decim == 4) { if (x4) FEMN(4, true); else FEMN(4, false); }
+        else { if (x4) FEMN(3, true); else FEMN(3, false); }
+#undef FEMN
 #undef FEM
     } else if (c->ntaps == 101 && in.rf_decim == 10) {
         FE2R(10);
