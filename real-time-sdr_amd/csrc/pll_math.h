@@ -161,4 +161,100 @@ PLLM_HD Phase phase_detect(float eI, float eQ, double c, double s, double mr, in
     return o;
 }
 
+// ------------------------------------------------------------------------------------------
+// v2 step (k_pll): shorter dependent chain and no f64 reciprocal inside the recurrence.
+//
+//  * rx = pll_rx(x): the PLL input's reciprocal, computed by the kernel that PRODUCES the input
+//    (it does not depend on the PLL state). f64 RN(1/x) with its two low mantissa bits replaced
+//    by 2*[x < 0] (a <= 3-ulp perturbation), or a NaN when |x| < 2^-60 or x is not finite.
+//  * sincos2_f32: the same reduction and kernels as sincos_f32, but kd comes from one fma with
+//    the 1.5*2^52 rounding constant, whose low word is q itself (no f64 -> int conversion).
+//  * phase_detect2: with (eI, eQ) = x * (RN c, -RN s), rotating by +t gives X = x (1 + delta),
+//    |delta| <= 2^-23, and Y = x c s (alpha + a - beta - b) for the four f32 rounding errors,
+//    so |Y / X| <= 2^-23 whenever |x| >= 2^-60 (subnormal products then only touch terms below
+//    2^-66). d = Y * rx replaces Y / X with an absolute error <= |d| (|delta| + 2^-51) < 2^-45.9,
+//    and atan2(eQ, eI) = base + d where base = -t + pi [x < 0] (mod 2pi) is prepared from the
+//    PREVIOUS step's quadrant before this step's input is touched (base_angle). EPS_ABS_E2 bounds
+//    the total absolute error (d, the reduction, base, the final add).
+// ------------------------------------------------------------------------------------------
+constexpr double MAGIC = 6755399441055744.0;   // 1.5 * 2^52: fma(x, c, MAGIC) - MAGIC = rint(x c)
+constexpr double EPS_ABS_E2 = 0x1p-44;
+
+PLLM_HD double pll_rx(float x) {
+    const float ax = __builtin_fabs(x);
+    if (!(ax >= 0x1p-60f) || !(ax <= 3.4028234663852886e38f))
+        return __builtin_bit_cast(double, (uint64_t)0x7FF8000000000000ull | (x < 0.0f ? 2u : 0u));
+    const double r = 1.0 / (double)x;
+    const uint64_t b = (__builtin_bit_cast(uint64_t, r) & ~(uint64_t)3) | (x < 0.0f ? 2u : 0u);
+    return __builtin_bit_cast(double, b);
+}
+
+struct SinCos2 {
+    double c, s;     // cos t, sin t (relative error < 2^-50)
+    double mr;       // -r, r = t - q*pi/2 in [-pi/4, pi/4]
+    uint32_t q;      // q (mod 2^32)
+    uint32_t b;      // [r < 0]
+    uint32_t tie;    // min(tie_distance64(c), tie_distance64(s)); (float)c, (float)s are RN_f32 when > 128
+};
+
+// valid for |t| < T_MAX (the caller checks the range)
+PLLM_HD SinCos2 sincos2_f32(float t) {
+    const double x = (double)t;
+    const double kdp = fma_(x, TWO_OVER_PI, MAGIC);
+    const double kd = kdp - MAGIC;
+    const uint32_t q = (uint32_t)__builtin_bit_cast(uint64_t, kdp);
+    double r = fma_(-kd, P1, x);
+    r = fma_(-kd, P2, r);
+    r = fma_(-kd, P3, r);
+    const double z = r * r;
+    const double z2 = z * z;
+    const double z4 = z2 * z2;
+    const double sp = fma_(z4, fma_(z, S6, S5), fma_(z2, fma_(z, S4, S3), fma_(z, S2, S1)));
+    const double sr = fma_(r * z, sp, r);
+    const double cp = fma_(z4, C5, fma_(z2, fma_(z, C4, C3), fma_(z, C2, C1)));
+    const double cr = fma_(z2, cp, fma_(z, -0.5, 1.0));
+    const bool swap = (q & 1u) != 0;
+    const double a = swap ? sr : cr;
+    const double bb = swap ? cr : sr;
+    SinCos2 o;
+    o.c = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, a) ^
+                                         ((uint64_t)(((q + 1u) << 30) & 0x80000000u) << 32));
+    o.s = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, bb) ^
+                                         ((uint64_t)((q << 30) & 0x80000000u) << 32));
+    o.mr = -r;
+    o.q = q;
+    o.b = (uint32_t)(__builtin_bit_cast(uint64_t, r) >> 63);
+    const uint32_t tc = tie_distance64(o.c), ts = tie_distance64(o.s);
+    o.tie = tc < ts ? tc : ts;
+    return o;
+}
+
+// -t + pi*[x < 0] (mod 2pi) as m*pi/2 + mr with m in {-2..1} chosen so the sum lies in [-pi, pi]:
+// with m0 = (2[x<0] - q) mod 4, m = ((m0 + b + 1) mod 4) - 1 - b (b = [mr > 0]; m0 = 2 picks +pi
+// when mr < 0 and -pi otherwise). nlo: low word of pll_rx(x) (bit 1 = [x < 0]).
+PLLM_HD double base_angle(uint32_t nlo, uint32_t q, uint32_t b, double mr) {
+    const int m = (int)((nlo - q + b + 1u) & 3u) - (int)(b + 1u);
+    return fma_((double)m, PIO2, mr);
+}
+
+struct Phase2 {
+    double e;        // atan2(eQ, eI), |error| <= EPS_ABS_E2 (NaN when rx is)
+    float ef;        // RN_f32(e)
+    uint32_t split;  // bits(RN_f32(e - eps)) ^ bits(RN_f32(e + eps)): 0 iff the f32 rounding is safe
+};
+
+PLLM_HD Phase2 phase_detect2(float eI, float eQ, double c, double s, double rx, double base) {
+    const double dI = (double)eI, dQ = (double)eQ;
+    const double Y = fma_(dI, s, dQ * c);
+    const double e = base + Y * rx;
+    Phase2 o;
+    o.e = e;
+    o.ef = (float)e;
+    o.split = __builtin_bit_cast(uint32_t, (float)(e - EPS_ABS_E2)) ^
+              __builtin_bit_cast(uint32_t, (float)(e + EPS_ABS_E2));
+    return o;
+}
+
+PLLM_HD uint32_t lo_word(double v) { return (uint32_t)__builtin_bit_cast(uint64_t, v); }
+
 }  // namespace pllm

@@ -742,7 +742,8 @@ __global__ __launch_bounds__(BLK) void k_fir(const float* __restrict__ x, size_t
                                              const float* __restrict__ hist, size_t hist_stride,
                                              const float* __restrict__ h0, const float* __restrict__ h1, int ntaps,
                                              int D, int ny, int tile, float* __restrict__ y0,
-                                             float* __restrict__ y1, size_t y_stride) {
+                                             float* __restrict__ y1, size_t y_stride,
+                                             double* __restrict__ rx0, size_t rx_stride) {
     extern __shared__ float4 smem4[];
     float* sh = reinterpret_cast<float*>(smem4);
     const int ntaps_pad = (ntaps + 3) & ~3;
@@ -774,6 +775,7 @@ __global__ __launch_bounds__(BLK) void k_fir(const float* __restrict__ x, size_t
         }
         y0[(size_t)ch * y_stride + n] = a0;
         if (NT == 2) y1[(size_t)ch * y_stride + n] = a1;
+        if (rx0) rx0[(size_t)ch * rx_stride + n] = pllm::pll_rx(a0);   // y0 feeds a PLL: its reciprocal
     }
 }
 
@@ -869,6 +871,9 @@ struct PllJob {
     // that block's output row (prev_out[ch][n]); the PLL kernel then never touches lastCarrier, so
     // the NCO of block b can run on another stream while the PLL of block b+1 runs.
     const float* prev_out;
+    // pll_math.h pll_rx of every input sample (written by the producer of `in`)
+    const double* rx;
+    size_t rx_stride;
 };
 struct PllJobs {
     PllJob j[2];
@@ -876,10 +881,17 @@ struct PllJobs {
 
 struct PllRegs {
     float fbI, fbQ, integ, ph;
-    double toff, c, s, mr;   // mr, q3: -t mod 2pi of the previous step's t (pll_math.h)
-    int q3;
+    double toff;
+    double c, s, mr;   // f64 cos, sin of the previous step's t and -r of its reduction
+    uint32_t q, b;     // its quadrant q and [r < 0] (pll_math.h sincos2_f32)
 };
 
+// The carried rotation (c, s, mr, q, b) is rebuilt from the state's previous trigArg
+// t = (float)(w*toff + phaseEst) (pll.cpp:47). The fast phase detector needs feedbackI/Q to be
+// RN_f32(cos t), RN_f32(sin t) of that same t -- true for any state this PLL (or the reference)
+// left behind and for the initial state (1, 0, toff 0, phase 0). Otherwise, or when t is out of
+// the reduction's range, mr is NaN: the first fast step yields a NaN and the chunk is redone
+// with libm fallbacks.
 __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
     PllRegs r;
     r.fbI = st.feedbackI;
@@ -887,63 +899,74 @@ __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
     r.integ = st.integrator;
     r.ph = st.phaseEst;
     r.toff = st.trigOffset;
-    // rotation reference for the phase detector: the previous step's trigArg (pll.cpp:47)
     const float t_prev = (float)(w * r.toff + (double)r.ph);
-    const pllm::SinCos sc = pllm::sincos_f32(t_prev);
+    const pllm::SinCos2 sc = pllm::sincos2_f32(t_prev);
     r.c = sc.c;
     r.s = sc.s;
-    r.mr = (__builtin_fabs((double)t_prev) < pllm::T_MAX) ? sc.mr : __builtin_nan("");
-    r.q3 = sc.q3;
+    r.q = sc.q;
+    r.b = sc.b;
+    const bool consistent = (__builtin_fabs((double)t_prev) < pllm::T_MAX) && sc.tie > 128u &&
+                            (float)sc.c == r.fbI && (float)sc.s == r.fbQ;
+    r.mr = consistent ? sc.mr : __builtin_nan("");
     return r;
 }
 
-// Per-chunk accumulators of the fast path's proof obligations (kept in VGPRs: no SGPR masks).
+// Per-chunk proof obligations of the fast path (VGPR accumulators, one check per chunk):
+//   * every phase-detector result is at least EPS_ABS_E2 from an f32 rounding boundary (split)
+//     and |e| < pi - 2^-30 (so the wrap to [-pi, pi] is the reference's),
+//   * every cos/sin is at least 64 f64 ulps from an f32 tie (tie),
+//   * the chunk ends with |phaseEst| < 2^28, |integrator| < 2^20 (finite: a NaN or inf from an
+//     invalid input -- pll_rx gives NaN for |x| < 2^-60 -- propagates into both) and
+//     |w| (|toff| + CHUNK) < 2^29, which bounds every |t| of the chunk below 2^30 (T_MAX).
 struct PllProof {
-    double dsum = 0.0;      // sum |residual angle|        needs < 2^-18 (a sum, so NaN/inf propagate:
-                            // X == 0 gives d = NaN, and a NaN e, t or phase can only come from a NaN d)
-    double emax = 0.0;      // max |e|                     needs < pi - 2^-30
-    double tmax = 0.0;      // max |t|                     needs < 2^30 (reduction range)
-    uint32_t split = 0u;    // OR of phase-detector rounding splits, needs 0
-    uint32_t tie = ~0u;     // min of sin/cos tie distances, needs > 128
-    __device__ __forceinline__ bool ok() const {
-        return (dsum < 0x1p-18) & (emax < pllm::PI - 0x1p-30) & (tmax < pllm::T_MAX) & (split == 0u) & (tie > 128u);
-    }
+    double emax = 0.0;
+    uint32_t split = 0u;
+    uint32_t tie = ~0u;
 };
 
-// one step; CHECKED: fall back to the f64 libm path whenever the fast path cannot prove the f32
-// rounding (used for chunk redo and short tails).
+__device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
+    return (pf.emax < pllm::PI - 0x1p-30) & (pf.split == 0u) & (pf.tie > 128u) &
+           (__builtin_fabs(r.ph) < 0x1p28f) & (__builtin_fabs(r.integ) < 0x1p20f) &
+           (__builtin_fabs(w) * (__builtin_fabs(r.toff) + (double)chunk) < 0x1p29);
+}
+
+// One step of pll.cpp:36-50. CHECKED: every result the fast path cannot prove is recomputed
+// with the f64 libm exactly as the reference (used for chunk redo and short tails).
 template <bool CHECKED>
-__device__ __forceinline__ void pll_step(PllRegs& r, float x, float Kp, float Ki, double w, float& t_out,
-                                         PllProof& pf) {
+__device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float Kp, float Ki, double w,
+                                         float& t_out, PllProof& pf) {
     const float eI = x * r.fbI;                               // pll.cpp:36
     const float eQ = x * (-r.fbQ);                            // pll.cpp:37
-    const pllm::Phase p = pllm::phase_detect(eI, eQ, r.c, r.s, r.mr, r.q3);
+    const double base = pllm::base_angle(pllm::lo_word(rx), r.q, r.b, r.mr);
+    const pllm::Phase2 p = pllm::phase_detect2(eI, eQ, r.c, r.s, rx, base);
     float e = p.ef;
-    if (CHECKED && !p.ok) e = (float)atan2((double)eQ, (double)eI);  // pll.cpp:39
+    if (CHECKED && !((__builtin_fabs(p.e) < pllm::PI - 0x1p-30) && p.split == 0u))
+        e = (float)atan2((double)eQ, (double)eI);             // pll.cpp:39
     r.integ = r.integ + Ki * e;                               // pll.cpp:41
     r.ph = r.ph + Kp * e + r.integ;                           // pll.cpp:42
     r.toff += 1.0;                                            // pll.cpp:46
     const float t = (float)(w * r.toff + (double)r.ph);       // pll.cpp:47
-    const pllm::SinCos sc = pllm::sincos_f32(t);
+    const pllm::SinCos2 sc = pllm::sincos2_f32(t);
     r.c = sc.c;
     r.s = sc.s;
     r.mr = sc.mr;
-    r.q3 = sc.q3;
+    r.q = sc.q;
+    r.b = sc.b;
     r.fbI = (float)sc.c;                                      // pll.cpp:49
     r.fbQ = (float)sc.s;                                      // pll.cpp:50
-    if (CHECKED && !sc.ok) {
-        double sv, cv;
-        sincos((double)t, &sv, &cv);
-        r.fbI = (float)cv;
-        r.fbQ = (float)sv;
-        r.c = cv;
-        r.s = sv;
-        if (!(__builtin_fabs((double)t) < pllm::T_MAX)) r.mr = __builtin_nan("");
-    }
-    if (!CHECKED) {
-        pf.dsum = pf.dsum + __builtin_fabs(p.d);
-        pf.emax = fmax(pf.emax, __builtin_fabs(p.e));      // NaN-ignoring max is fine: see dsum
-        pf.tmax = fmax(pf.tmax, __builtin_fabs((double)t));
+    if (CHECKED) {
+        const bool in_range = __builtin_fabs((double)t) < pllm::T_MAX;
+        if (!(in_range && sc.tie > 128u)) {
+            double sv, cv;
+            sincos((double)t, &sv, &cv);
+            r.fbI = (float)cv;
+            r.fbQ = (float)sv;
+            r.c = cv;
+            r.s = sv;
+            if (!in_range) r.mr = __builtin_nan("");
+        }
+    } else {
+        pf.emax = fmax(pf.emax, __builtin_fabs(p.e));
         pf.split |= p.split;
         pf.tie = min(pf.tie, sc.tie);
     }
@@ -952,9 +975,9 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, float Kp, float Ki
 
 constexpr int PLL_CHUNK = 16;
 
-// VEC: x rows and the t buffer are 16-byte aligned with strides that are multiples of 4, so a
-// chunk's inputs are prefetched with float4 loads one chunk ahead and the 16 phases are stored
-// with float4 stores -- the unrolled chunk itself touches no memory.
+// VEC: x / rx rows and the t buffer are 16-byte aligned with strides that are multiples of 4
+// (x, t) and 2 (rx), so a chunk's inputs are prefetched with 16-byte loads one chunk ahead and
+// the 16 phases are stored with 16-byte stores -- the unrolled chunk itself touches no memory.
 template <bool VEC>
 __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) {
     const int ch = blockIdx.x * blockDim.x + threadIdx.x;
@@ -975,38 +998,47 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) 
     const double w = 2 * 3.14159265358979323846 * (freq / Fs);
     const sdr_pll_state s0 = st[ch];
     const float* x = in + (size_t)ch * in_stride;
+    const double* rxp = jb.rx + (size_t)ch * jb.rx_stride;
     float* tb = tbuf + (size_t)ch * t_stride;
     if (!jb.prev_out) out[(size_t)ch * out_stride] = s0.lastCarrier;   // pll.cpp:18
     PllRegs r = pll_load(s0, w);
-    // chunks of PLL_CHUNK steps run the unchecked fast path; inputs of the next chunk are loaded
-    // while the current one computes (float4 when rows are 16-byte aligned, VEC)
     const int nfull = (n / PLL_CHUNK) * PLL_CHUNK;
     float xa[PLL_CHUNK];
-    auto load_chunk = [&](float* dst, int i0) {
+    double ra[PLL_CHUNK];
+    auto load_chunk = [&](float* dx, double* dr, int i0) {
         if (VEC) {
 #pragma unroll
             for (int k = 0; k < PLL_CHUNK / 4; k++) {
                 const float4 v = reinterpret_cast<const float4*>(x + i0)[k];
-                dst[4 * k] = v.x; dst[4 * k + 1] = v.y; dst[4 * k + 2] = v.z; dst[4 * k + 3] = v.w;
+                dx[4 * k] = v.x; dx[4 * k + 1] = v.y; dx[4 * k + 2] = v.z; dx[4 * k + 3] = v.w;
+            }
+#pragma unroll
+            for (int k = 0; k < PLL_CHUNK / 2; k++) {
+                const double2 v = reinterpret_cast<const double2*>(rxp + i0)[k];
+                dr[2 * k] = v.x; dr[2 * k + 1] = v.y;
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK; k++) dst[k] = x[i0 + k];
+            for (int k = 0; k < PLL_CHUNK; k++) {
+                dx[k] = x[i0 + k];
+                dr[k] = rxp[i0 + k];
+            }
         }
     };
-    if (nfull > 0) load_chunk(xa, 0);
+    if (nfull > 0) load_chunk(xa, ra, 0);
     for (int i0 = 0; i0 < nfull; i0 += PLL_CHUNK) {
         float xn[PLL_CHUNK];
+        double rn[PLL_CHUNK];
         const bool more = i0 + PLL_CHUNK < nfull;
-        if (more) load_chunk(xn, i0 + PLL_CHUNK);
+        if (more) load_chunk(xn, rn, i0 + PLL_CHUNK);
         const PllRegs snap = r;
         PllProof pf;
         float tv[PLL_CHUNK];
 #pragma unroll
-        for (int j = 0; j < PLL_CHUNK; j++) pll_step<false>(r, xa[j], Kp, Ki, w, tv[j], pf);
-        if (!pf.ok()) {
+        for (int j = 0; j < PLL_CHUNK; j++) pll_step<false>(r, xa[j], ra[j], Kp, Ki, w, tv[j], pf);
+        if (!pll_chunk_ok(pf, r, w, PLL_CHUNK)) {
             r = snap;
-            for (int j = 0; j < PLL_CHUNK; j++) pll_step<true>(r, x[i0 + j], Kp, Ki, w, tb[i0 + j], pf);
+            for (int j = 0; j < PLL_CHUNK; j++) pll_step<true>(r, x[i0 + j], rxp[i0 + j], Kp, Ki, w, tb[i0 + j], pf);
         } else if (VEC) {
 #pragma unroll
             for (int k = 0; k < PLL_CHUNK / 4; k++)
@@ -1017,12 +1049,15 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) 
         }
         if (more) {
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK; k++) xa[k] = xn[k];
+            for (int k = 0; k < PLL_CHUNK; k++) {
+                xa[k] = xn[k];
+                ra[k] = rn[k];
+            }
         }
     }
     {
         PllProof pf;
-        for (int i = nfull; i < n; i++) pll_step<true>(r, x[i], Kp, Ki, w, tb[i], pf);
+        for (int i = nfull; i < n; i++) pll_step<true>(r, x[i], rxp[i], Kp, Ki, w, tb[i], pf);
     }
     // every field but lastCarrier (k_nco_out's)
     st[ch].feedbackI = r.fbI;
@@ -1030,6 +1065,14 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) 
     st[ch].integrator = r.integ;
     st[ch].phaseEst = r.ph;
     st[ch].trigOffset = r.toff;
+}
+
+// pll_rx of a PLL input with no fused producer (the batched sdr_fmpll primitive)
+__global__ __launch_bounds__(BLK) void k_pll_rx(double* __restrict__ rx, size_t rx_stride, const float* __restrict__ x,
+                                                size_t x_stride, int n) {
+    const int ch = blockIdx.y;
+    const int i = blockIdx.x * BLK + threadIdx.x;
+    if (i < n) rx[(size_t)ch * rx_stride + i] = pllm::pll_rx(x[(size_t)ch * x_stride + i]);
 }
 
 __global__ __launch_bounds__(64) void k_pll_libm(const PllJobs jobs, int n, int nch) {
@@ -1415,7 +1458,8 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
     for (int k = 0; k < njobs; k++) {
         const PllJob& j = jobs.j[k];
         vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
-              (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0);
+              (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
+              (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0);
     }
     if (libm || pll_libm_env()) {
         hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, jobs, n, nch);
@@ -1429,10 +1473,15 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
 }
 
 int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
-               size_t t_stride, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale, float phaseAdjust,
-               float bw, hipStream_t s) {
+               size_t t_stride, double* rxbuf, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale,
+               float phaseAdjust, float bw, hipStream_t s) {
+    if (n > 0) {
+        hipLaunchKernelGGL(k_pll_rx, dim3(cdiv(n, BLK), nch), dim3(BLK), 0, s, rxbuf, t_stride, in, in_stride, n);
+        LAUNCH_CHECK();
+    }
     PllJobs jobs{};
-    jobs.j[0] = PllJob{in, in_stride, tbuf, t_stride, out, out_stride, st, freq, Fs, bw, ncoScale, phaseAdjust, nullptr};
+    jobs.j[0] = PllJob{in, in_stride, tbuf, t_stride, out, out_stride, st, freq, Fs, bw, ncoScale, phaseAdjust, nullptr,
+                       rxbuf, t_stride};
     return launch_plls(libm, jobs, 1, n, nch, s);
 }
 
@@ -1459,6 +1508,8 @@ struct sdr_ctx {
     // plain per-block buffers
     float *pilot = nullptr, *band = nullptr, *gpilot = nullptr, *carrier = nullptr, *ipll = nullptr,
           *rds_clean = nullptr, *t_st = nullptr, *t_rds = nullptr;
+    double *rx_st = nullptr, *rx_rds = nullptr;         // PLL input reciprocals (pll_math.h pll_rx),
+                                                        // [2 parities][nch][plain_stride], from the FIRs
     size_t plain_stride = 0, pll_stride = 0, clean_stride = 0;
     size_t plain_par = 0, pll_par = 0;                  // pilot/band/gpilot and carrier/ipll are
                                                         // [2 parities][nch][...] so that the stages
@@ -1486,6 +1537,7 @@ struct sdr_ctx {
     float* ext(float* base, size_t par, int p) const { return base + p * par; }
     float* plain(float* base) const { return base + parity * plain_par; }
     float* pllbuf(float* base) const { return base + parity * pll_par; }
+    double* rxbuf(double* base) const { return base + parity * plain_par; }
 };
 
 namespace {
@@ -1578,13 +1630,13 @@ PllJob stereo_job(sdr_ctx* c) {   // stereo.cpp:77: fmpll(pilot, 19e3, rf_Fs/rf_
     const sdr_info& in = c->info;
     return PllJob{c->plain(c->pilot), c->plain_stride, c->plain(c->t_st), c->plain_stride, c->pllbuf(c->carrier),
                   c->pll_stride, c->st_pll, 19e3f, (float)(in.rf_Fs / in.rf_decim), 0.01f, 2.0f, 0.0f,
-                  c->carrier + (c->parity ^ 1) * c->pll_par};
+                  c->carrier + (c->parity ^ 1) * c->pll_par, c->rxbuf(c->rx_st), c->plain_stride};
 }
 PllJob rds_job(sdr_ctx* c) {      // rds.cpp:119: fmpll(gen_pilot, 114e3, if_Fs, ..., 0.5, 0, 0.001)
     const sdr_info& in = c->info;
     return PllJob{c->plain(c->gpilot), c->plain_stride, c->plain(c->t_rds), c->plain_stride, c->pllbuf(c->ipll),
                   c->pll_stride, c->rds_pll, 114e3f, (float)in.if_Fs, 0.001f, 0.5f, 0.0f,
-                  c->ipll + (c->parity ^ 1) * c->pll_par};
+                  c->ipll + (c->parity ^ 1) * c->pll_par, c->rxbuf(c->rx_rds), c->plain_stride};
 }
 
 }  // namespace
@@ -1720,6 +1772,8 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     TRY(dalloc(c, &c->gpilot, 2 * c->plain_par));
     TRY(dalloc(c, &c->t_st, 2 * c->plain_par));
     TRY(dalloc(c, &c->t_rds, 2 * c->plain_par));
+    TRY(dalloc(c, &c->rx_st, 2 * c->plain_par));
+    TRY(dalloc(c, &c->rx_rds, 2 * c->plain_par));
     TRY(dalloc(c, &c->carrier, 2 * c->pll_par));
     TRY(dalloc(c, &c->ipll, 2 * c->pll_par));
     TRY(dalloc(c, &c->rds_clean, c->clean_stride * nch));
@@ -1875,7 +1929,7 @@ int sdr_stereo_pre(sdr_ctx* c, void* stream) {
     dim3 gf(cdiv(n, FIR_TILE), c->nch);
     hipLaunchKernelGGL((k_fir<2, false>), gf, dim3(BLK), fir_lds_bytes(T, 2, FIR_TILE, 1), S(stream), fm,
                        c->fm_stride, fm, c->fm_stride, c->pilot_h, c->stereo_h, T, 1, n, FIR_TILE, c->plain(c->pilot),
-                       c->plain(c->band), c->plain_stride);
+                       c->plain(c->band), c->plain_stride, c->rxbuf(c->rx_st), c->plain_stride);
     LAUNCH_CHECK();
     c->st_pre_done = c->block;
     return SDR_OK;
@@ -1950,12 +2004,12 @@ int sdr_rds_pre(sdr_ctx* c, void* stream) {
                        c->fm_stride, n);
     LAUNCH_CHECK();
     hipLaunchKernelGGL((k_fir<1, false>), gf, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, fm, c->fm_stride, fm,
-                       c->fm_stride, c->rds_h, nullptr, T, 1, n, FIR_TILE, rband, nullptr, c->fm_stride);
+                       c->fm_stride, c->rds_h, nullptr, T, 1, n, FIR_TILE, rband, nullptr, c->fm_stride, nullptr, 0);
     LAUNCH_CHECK();
     // squaring (:111-113) + 114 kHz BPF (:116)
     hipLaunchKernelGGL((k_fir<1, true>), gf, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, rband, c->fm_stride,
                        rband, c->fm_stride, c->rds_sq_h, nullptr, T, 1, n, FIR_TILE, c->plain(c->gpilot), nullptr,
-                       c->plain_stride);
+                       c->plain_stride, c->rxbuf(c->rx_rds), c->plain_stride);
     LAUNCH_CHECK();
     c->rds_pre_done = c->block;
     return SDR_OK;
@@ -2022,7 +2076,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
     float* dst = rds_clean ? rds_clean : c->rds_clean;
     const size_t dst_stride = rds_clean ? rds_stride : c->clean_stride;
     hipLaunchKernelGGL((k_fir<1, false>), gc, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, rfilt, c->rf_stride,
-                       rfilt, c->rf_stride, c->rrc_h, nullptr, T, 1, in.n_rds, FIR_TILE, dst, nullptr, dst_stride);
+                       rfilt, c->rf_stride, c->rrc_h, nullptr, T, 1, in.n_rds, FIR_TILE, dst, nullptr, dst_stride, nullptr, 0);
     LAUNCH_CHECK();
     if (rds_clean) {
         HIP_TRY(hipMemcpy2DAsync(c->rds_clean, c->clean_stride * sizeof(float), rds_clean, rds_stride * sizeof(float),
@@ -2094,7 +2148,7 @@ int sdr_convolve_fir(float* y, size_t y_stride, const float* x, size_t x_stride,
         const size_t lds = fir_lds_bytes(ntaps, 1, tile, D);
         if (lds > 160 * 1024) return fail(SDR_E_INVALID, "convolve_fir: ntaps*D too large for one tile");
         hipLaunchKernelGGL((k_fir<1, false>), dim3(cdiv(ny, tile), nch), dim3(BLK), lds, S(stream), x, x_stride,
-                           state + nstate, (size_t)nstate, h, nullptr, ntaps, D, ny, tile, y, nullptr, y_stride);
+                           state + nstate, (size_t)nstate, h, nullptr, ntaps, D, ny, tile, y, nullptr, y_stride, nullptr, 0);
         LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_state_update, dim3(nch), dim3(256), 0, S(stream), state, nstate, x, x_stride, nx);
@@ -2184,11 +2238,18 @@ int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, 
               sdr_pll_state* state, float ncoScale, float phaseAdjust, float normBandwidth, void* stream) {
     if (!out || !in || !state || nch <= 0 || n < 0) return fail(SDR_E_INVALID, "fmpll: bad arguments");
     const size_t ts = round_up((size_t)std::max(n, 1), 4);
-    float* tbuf = nullptr;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tbuf), ts * nch * sizeof(float), S(stream)));
-    const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, tbuf, ts, out, out_stride, state, ncoScale,
+    // one scratch allocation: the input reciprocals [nch][ts] f64, then the phases [nch][ts] f32.
+    // Plain hipMalloc/hipFree (hipFree waits for the kernels): with two stream-ordered
+    // hipMallocAsync/hipFreeAsync pairs per call the drop-in harness saw non-deterministic PLL
+    // outputs on ROCm 7.2 (tools/diag_dropin_pll.py), so this primitive stays synchronous.
+    void* scratch = nullptr;
+    HIP_TRY(hipMalloc(&scratch, ts * nch * (sizeof(double) + sizeof(float))));
+    double* rxbuf = static_cast<double*>(scratch);
+    float* tbuf = reinterpret_cast<float*>(rxbuf + ts * nch);
+    const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, tbuf, ts, rxbuf, out, out_stride, state, ncoScale,
                              phaseAdjust, normBandwidth, S(stream));
-    HIP_TRY(hipFreeAsync(tbuf, S(stream)));
+    HIP_TRY(hipStreamSynchronize(S(stream)));
+    HIP_TRY(hipFree(scratch));
     return r;
 }
 

@@ -38,6 +38,26 @@ CHAIN(i_fma_f32, float, "v_fma_f32 %0, %0, %4, %5\n v_fma_f32 %1, %1, %4, %5\n v
 CHAIN(i_mul_f64, double, "v_mul_f64 %0, %0, %4\n v_mul_f64 %1, %1, %4\n v_mul_f64 %2, %2, %4\n v_mul_f64 %3, %3, %4",
       "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "v"(a))
 
+CHAIN(i_add_f64, double, "v_add_f64 %0, %0, %4\n v_add_f64 %1, %1, %4\n v_add_f64 %2, %2, %4\n v_add_f64 %3, %3, %4",
+      "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "v"(a))
+CHAIN(i_rcp_f64, double, "v_rcp_f64 %0, %0\n v_rcp_f64 %1, %1\n v_rcp_f64 %2, %2\n v_rcp_f64 %3, %3",
+      "+v"(x), "+v"(y), "+v"(z), "+v"(w))
+CHAIN(i_rndne_f64, double, "v_rndne_f64 %0, %0\n v_rndne_f64 %1, %1\n v_rndne_f64 %2, %2\n v_rndne_f64 %3, %3",
+      "+v"(x), "+v"(y), "+v"(z), "+v"(w))
+CHAIN(i_xor_b32, float, "v_xor_b32 %0, %0, %4\n v_xor_b32 %1, %1, %4\n v_xor_b32 %2, %2, %4\n v_xor_b32 %3, %3, %4",
+      "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "v"(a))
+CHAIN(i_cvt_f64_f32, double, "v_cvt_f64_f32 %0, %4\n v_cvt_f64_f32 %1, %4\n v_cvt_f64_f32 %2, %4\n v_cvt_f64_f32 %3, %4",
+      "=v"(x), "=v"(y), "=v"(z), "=v"(w) : "v"((float)a))
+CHAIN(i_cvt_f32_f64, float, "v_cvt_f32_f64 %0, %4\n v_cvt_f32_f64 %1, %4\n v_cvt_f32_f64 %2, %4\n v_cvt_f32_f64 %3, %4",
+      "=v"(x), "=v"(y), "=v"(z), "=v"(w) : "v"((double)a))
+CHAIN(i_pk_mul_f32, double, "v_pk_mul_f32 %0, %0, %4\n v_pk_mul_f32 %1, %1, %4\n v_pk_mul_f32 %2, %2, %4\n v_pk_mul_f32 %3, %3, %4",
+      "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "v"(a))
+CHAIN(i_mix_f64_f32, double, "v_fma_f64 %0, %0, %4, %4\n v_xor_b32 %5, %5, %5\n v_fma_f64 %1, %1, %4, %4\n v_xor_b32 %6, %6, %6",
+      "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "v"(a), "v"(0), "v"(1))
+CHAIN(i_mov_dpp, float, "v_mov_b32_dpp %0, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n v_mov_b32_dpp %1, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n v_mov_b32_dpp %2, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n v_mov_b32_dpp %3, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf",
+      "=v"(x), "=v"(y), "=v"(z), "=v"(w) : "v"(a))
+CHAIN(d_cvt_rt, float, "v_cvt_f64_f32 v[40:41], %0\n v_cvt_f32_f64 %0, v[40:41]", "+v"(x) : : "v40", "v41")
+
 template <typename TY>
 void run(void (*k)(TY*, long long*, TY, TY), const char* name, int per_iter) {
     TY* o;
@@ -70,5 +90,15 @@ int main() {
     run(i_fma_f64, "ind fma_f64", 4);
     run(i_fma_f32, "ind fma_f32", 4);
     run(i_mul_f64, "ind mul_f64", 4);
+    run(i_add_f64, "ind add_f64", 4);
+    run(i_rcp_f64, "ind rcp_f64", 4);
+    run(i_rndne_f64, "ind rndne_f64", 4);
+    run(i_xor_b32, "ind xor_b32", 4);
+    run(i_cvt_f64_f32, "ind cvt64_32", 4);
+    run(i_cvt_f32_f64, "ind cvt32_64", 4);
+    run(i_pk_mul_f32, "ind pk_mul", 4);
+    run(i_mix_f64_f32, "ind fma64+xor", 4);
+    run(i_mov_dpp, "ind mov_dpp", 4);
+    run(d_cvt_rt, "dep cvt 64<-32->", 2);
     return 0;
 }
