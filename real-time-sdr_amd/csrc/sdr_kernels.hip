@@ -930,6 +930,11 @@ __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& 
            (__builtin_fabs(w) * (__builtin_fabs(r.toff) + (double)chunk) < 0x1p29);
 }
 
+// the f64 libm of the reference step (pll.cpp:39, :49-50), out of line: only the rare fallbacks
+// call them, and the unrolled redo chunks stay small
+__device__ __noinline__ float pll_atan2_ref(float eQ, float eI) { return (float)atan2((double)eQ, (double)eI); }
+__device__ __noinline__ void pll_sincos_ref(float t, double* s, double* c) { sincos((double)t, s, c); }
+
 // One step of pll.cpp:36-50. CHECKED: every result the fast path cannot prove is recomputed
 // with the f64 libm exactly as the reference (used for chunk redo and short tails).
 template <bool CHECKED>
@@ -941,7 +946,7 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
     const pllm::Phase2 p = pllm::phase_detect2(eI, eQ, r.c, r.s, rx, base);
     float e = p.ef;
     if (CHECKED && !((__builtin_fabs(p.e) < pllm::PI - 0x1p-30) && p.split == 0u))
-        e = (float)atan2((double)eQ, (double)eI);             // pll.cpp:39
+        e = pll_atan2_ref(eQ, eI);                            // pll.cpp:39
     r.integ = r.integ + Ki * e;                               // pll.cpp:41
     r.ph = r.ph + Kp * e + r.integ;                           // pll.cpp:42
     r.toff += 1.0;                                            // pll.cpp:46
@@ -958,7 +963,7 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
         const bool in_range = __builtin_fabs((double)t) < pllm::T_MAX;
         if (!(in_range && sc.tie > 128u)) {
             double sv, cv;
-            sincos((double)t, &sv, &cv);
+            pll_sincos_ref(t, &sv, &cv);
             r.fbI = (float)cv;
             r.fbQ = (float)sv;
             r.c = cv;
@@ -974,6 +979,10 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
 }
 
 constexpr int PLL_CHUNK = 16;
+#ifndef SDR_PLL_NBUF
+#define SDR_PLL_NBUF 3
+#endif
+constexpr int PLL_NBUF = SDR_PLL_NBUF;   // register buffers of inputs (prefetch distance NBUF - 1 chunks)
 
 // VEC: x / rx rows and the t buffer are 16-byte aligned with strides that are multiples of 4
 // (x, t) and 2 (rx), so a chunk's inputs are prefetched with 16-byte loads one chunk ahead and
@@ -1002,62 +1011,69 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) 
     float* tb = tbuf + (size_t)ch * t_stride;
     if (!jb.prev_out) out[(size_t)ch * out_stride] = s0.lastCarrier;   // pll.cpp:18
     PllRegs r = pll_load(s0, w);
-    const int nfull = (n / PLL_CHUNK) * PLL_CHUNK;
-    float xa[PLL_CHUNK];
-    double ra[PLL_CHUNK];
+    // Chunks rotate through PLL_NBUF register buffers: chunk c computes from buffer c % NBUF, stores
+    // its phases, then refills that buffer with chunk c + NBUF. A chunk's inputs are thus loaded
+    // NBUF - 1 chunks ahead and, being issued after the previous chunk's stores, never make a
+    // wait include those stores (vmcnt counts loads and stores in issue order). The main loop
+    // covers a multiple of NBUF chunks; the rest (< NBUF chunks + n % CHUNK) runs checked steps.
+    constexpr int C = PLL_CHUNK, NB = PLL_NBUF;
+    const int nchunks = n / C;
+    const int nmain = nchunks - nchunks % NB;
+    float xb[NB][C];
+    double rb[NB][C];
     auto load_chunk = [&](float* dx, double* dr, int i0) {
         if (VEC) {
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK / 4; k++) {
+            for (int k = 0; k < C / 4; k++) {
                 const float4 v = reinterpret_cast<const float4*>(x + i0)[k];
                 dx[4 * k] = v.x; dx[4 * k + 1] = v.y; dx[4 * k + 2] = v.z; dx[4 * k + 3] = v.w;
             }
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK / 2; k++) {
+            for (int k = 0; k < C / 2; k++) {
                 const double2 v = reinterpret_cast<const double2*>(rxp + i0)[k];
                 dr[2 * k] = v.x; dr[2 * k + 1] = v.y;
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK; k++) {
+            for (int k = 0; k < C; k++) {
                 dx[k] = x[i0 + k];
                 dr[k] = rxp[i0 + k];
             }
         }
     };
-    if (nfull > 0) load_chunk(xa, ra, 0);
-    for (int i0 = 0; i0 < nfull; i0 += PLL_CHUNK) {
-        float xn[PLL_CHUNK];
-        double rn[PLL_CHUNK];
-        const bool more = i0 + PLL_CHUNK < nfull;
-        if (more) load_chunk(xn, rn, i0 + PLL_CHUNK);
-        const PllRegs snap = r;
-        PllProof pf;
-        float tv[PLL_CHUNK];
+    if (nmain > 0) {
 #pragma unroll
-        for (int j = 0; j < PLL_CHUNK; j++) pll_step<false>(r, xa[j], ra[j], Kp, Ki, w, tv[j], pf);
-        if (!pll_chunk_ok(pf, r, w, PLL_CHUNK)) {
-            r = snap;
-            for (int j = 0; j < PLL_CHUNK; j++) pll_step<true>(r, x[i0 + j], rxp[i0 + j], Kp, Ki, w, tb[i0 + j], pf);
-        } else if (VEC) {
+        for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
+    }
+    for (int c0 = 0; c0 < nmain; c0 += NB) {
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK / 4; k++)
-                reinterpret_cast<float4*>(tb + i0)[k] = make_float4(tv[4 * k], tv[4 * k + 1], tv[4 * k + 2], tv[4 * k + 3]);
-        } else {
+        for (int u = 0; u < NB; u++) {
+            const int i0 = (c0 + u) * C;
+            const PllRegs snap = r;
+            PllProof pf;
+            float tv[C];
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK; k++) tb[i0 + k] = tv[k];
-        }
-        if (more) {
+            for (int j = 0; j < C; j++) pll_step<false>(r, xb[u][j], rb[u][j], Kp, Ki, w, tv[j], pf);
+            if (!pll_chunk_ok(pf, r, w, C)) {
+                r = snap;
 #pragma unroll
-            for (int k = 0; k < PLL_CHUNK; k++) {
-                xa[k] = xn[k];
-                ra[k] = rn[k];
+                for (int j = 0; j < C; j++) pll_step<true>(r, xb[u][j], rb[u][j], Kp, Ki, w, tv[j], pf);
             }
+            if (VEC) {
+#pragma unroll
+                for (int k = 0; k < C / 4; k++)
+                    reinterpret_cast<float4*>(tb + i0)[k] = make_float4(tv[4 * k], tv[4 * k + 1], tv[4 * k + 2], tv[4 * k + 3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
+            }
+            // refill (the last refills re-read the final chunk: harmless, keeps the loop branch-free)
+            load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
         }
     }
     {
         PllProof pf;
-        for (int i = nfull; i < n; i++) pll_step<true>(r, x[i], rxp[i], Kp, Ki, w, tb[i], pf);
+        for (int i = nmain * C; i < n; i++) pll_step<true>(r, x[i], rxp[i], Kp, Ki, w, tb[i], pf);
     }
     // every field but lastCarrier (k_nco_out's)
     st[ch].feedbackI = r.fbI;
