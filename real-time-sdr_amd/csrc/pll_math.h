@@ -246,7 +246,7 @@ struct Phase2 {
 PLLM_HD Phase2 phase_detect2(float eI, float eQ, double c, double s, double rx, double base) {
     const double dI = (double)eI, dQ = (double)eQ;
     const double Y = fma_(dI, s, dQ * c);
-    const double e = base + Y * rx;
+    const double e = fma_(Y, rx, base);   // base + d with one rounding
     Phase2 o;
     o.e = e;
     o.ef = (float)e;
@@ -256,5 +256,63 @@ PLLM_HD Phase2 phase_detect2(float eI, float eQ, double c, double s, double rx, 
 }
 
 PLLM_HD uint32_t lo_word(double v) { return (uint32_t)__builtin_bit_cast(uint64_t, v); }
+
+// ------------------------------------------------------------------------------------------
+// Reduced-frame step (k_pll). With t = q pi/2 + r, cos t + i sin t = i^q (cos r + i sin r), and
+// RN_f32 commutes with multiplying by i^q (it only swaps and negates components), so
+//   fbI + i fbQ = i^q (fI0 + i fQ0),  fI0 = RN(cos r), fQ0 = RN(sin r)            (pll.cpp:49-50)
+//   eI - i eQ   = i^q (eI0 - i eQ0),  eI0 = RN(x fI0), eQ0 = RN(-x fQ0)           (pll.cpp:36-37)
+// and the rotated residual X + iY = (eI + i eQ)(c + i s) equals (eI0 + i eQ0)(cos r + i sin r).
+// The recurrence therefore never needs the quadrant swap/sign of cos t, sin t: it carries
+// (fI0, fQ0) and q, and the quadrant enters only through base_angle. rot_q applies i^q to a pair
+// (exactly), for the state at block boundaries and for the libm fallbacks.
+// ------------------------------------------------------------------------------------------
+struct SinCosR {
+    double cr, sr;   // cos r, sin r (relative error < 2^-50)
+    double mr;       // -r
+    uint32_t q, b;   // quadrant, [r < 0]
+    uint32_t tie;    // min(tie_distance64(cr), tie_distance64(sr))
+};
+
+// valid for |t| < T_MAX (the caller checks the range)
+PLLM_HD SinCosR sincos_r(float t) {
+    const double x = (double)t;
+    const double kdp = fma_(x, TWO_OVER_PI, MAGIC);
+    const double kd = kdp - MAGIC;
+    double r = fma_(-kd, P1, x);
+    r = fma_(-kd, P2, r);
+    r = fma_(-kd, P3, r);
+    const double z = r * r;
+    const double z2 = z * z;
+    const double z4 = z2 * z2;
+    const double sp = fma_(z4, fma_(z, S6, S5), fma_(z2, fma_(z, S4, S3), fma_(z, S2, S1)));
+    const double cp = fma_(z4, C5, fma_(z2, fma_(z, C4, C3), fma_(z, C2, C1)));
+    SinCosR o;
+    o.sr = fma_(r * z, sp, r);
+    o.cr = fma_(z2, cp, fma_(z, -0.5, 1.0));
+    o.mr = -r;
+    o.q = (uint32_t)__builtin_bit_cast(uint64_t, kdp);
+    o.b = (uint32_t)(__builtin_bit_cast(uint64_t, r) >> 63);
+    const uint32_t tc = tie_distance64(o.cr), ts = tie_distance64(o.sr);
+    o.tie = tc < ts ? tc : ts;
+    return o;
+}
+
+// (a, b) <- i^q (a + i b): q mod 4 = 1 -> (-b, a), 2 -> (-a, -b), 3 -> (b, -a)
+template <typename T>
+PLLM_HD void rot_q(uint32_t q, T& a, T& b) {
+    const T a0 = a, b0 = b;
+    switch (q & 3u) {
+        case 1: a = -b0; b = a0; break;
+        case 2: a = -a0; b = -b0; break;
+        case 3: a = b0; b = -a0; break;
+        default: break;
+    }
+}
+
+// the residual angle of the reduced frame (same value as phase_detect2's, see above)
+PLLM_HD Phase2 phase_detect_r(float eI0, float eQ0, double cr, double sr, double rx, double base) {
+    return phase_detect2(eI0, eQ0, cr, sr, rx, base);
+}
 
 }  // namespace pllm

@@ -880,34 +880,46 @@ struct PllJobs {
 };
 
 struct PllRegs {
-    float fbI, fbQ, integ, ph;
+    float fbI, fbQ, integ, ph;   // fbI, fbQ in the reduced frame: RN(cos r), RN(sin r) (pll_math.h)
     double toff;
-    double c, s, mr;   // f64 cos, sin of the previous step's t and -r of its reduction
-    uint32_t q, b;     // its quadrant q and [r < 0] (pll_math.h sincos2_f32)
+    double c, s, mr;             // f64 cos r, sin r and -r of the previous step's t = q pi/2 + r
+    uint32_t q, b;               // its quadrant q and [r < 0]
 };
 
-// The carried rotation (c, s, mr, q, b) is rebuilt from the state's previous trigArg
-// t = (float)(w*toff + phaseEst) (pll.cpp:47). The fast phase detector needs feedbackI/Q to be
-// RN_f32(cos t), RN_f32(sin t) of that same t -- true for any state this PLL (or the reference)
-// left behind and for the initial state (1, 0, toff 0, phase 0). Otherwise, or when t is out of
-// the reduction's range, mr is NaN: the first fast step yields a NaN and the chunk is redone
-// with libm fallbacks.
+// The carried rotation is rebuilt from the state's previous trigArg t = (float)(w*toff + phaseEst)
+// (pll.cpp:47). The fast phase detector needs feedbackI/Q to be RN_f32(cos t), RN_f32(sin t) of
+// that same t -- true for any state this PLL (or the reference) left behind and for the initial
+// state (1, 0, toff 0, phase 0). Otherwise, or when t is out of the reduction's range, the
+// feedback is kept as given with q = 0 and mr = NaN: the first fast step yields a NaN and the
+// chunk is redone with libm fallbacks, which use the state's feedback exactly.
 __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
     PllRegs r;
-    r.fbI = st.feedbackI;
-    r.fbQ = st.feedbackQ;
     r.integ = st.integrator;
     r.ph = st.phaseEst;
     r.toff = st.trigOffset;
     const float t_prev = (float)(w * r.toff + (double)r.ph);
-    const pllm::SinCos2 sc = pllm::sincos2_f32(t_prev);
-    r.c = sc.c;
-    r.s = sc.s;
-    r.q = sc.q;
-    r.b = sc.b;
+    const pllm::SinCosR sc = pllm::sincos_r(t_prev);
+    float fI = (float)sc.cr, fQ = (float)sc.sr;
+    pllm::rot_q(sc.q, fI, fQ);
     const bool consistent = (__builtin_fabs((double)t_prev) < pllm::T_MAX) && sc.tie > 128u &&
-                            (float)sc.c == r.fbI && (float)sc.s == r.fbQ;
-    r.mr = consistent ? sc.mr : __builtin_nan("");
+                            fI == st.feedbackI && fQ == st.feedbackQ;
+    if (consistent) {
+        r.fbI = (float)sc.cr;
+        r.fbQ = (float)sc.sr;
+        r.c = sc.cr;
+        r.s = sc.sr;
+        r.mr = sc.mr;
+        r.q = sc.q;
+        r.b = sc.b;
+    } else {
+        r.fbI = st.feedbackI;
+        r.fbQ = st.feedbackQ;
+        r.c = 1.0;
+        r.s = 0.0;
+        r.mr = __builtin_nan("");
+        r.q = 0u;
+        r.b = 0u;
+    }
     return r;
 }
 
@@ -924,10 +936,12 @@ struct PllProof {
     uint32_t tie = ~0u;
 };
 
+// TAB: the trigArg offsets come from a table whose range the kernel checked once (pll_run)
+template <bool TAB>
 __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
     return (pf.emax < pllm::PI - 0x1p-30) & (pf.split == 0u) & (pf.tie > 128u) &
            (__builtin_fabs(r.ph) < 0x1p28f) & (__builtin_fabs(r.integ) < 0x1p20f) &
-           (__builtin_fabs(w) * (__builtin_fabs(r.toff) + (double)chunk) < 0x1p29);
+           (TAB || (__builtin_fabs(w) * (__builtin_fabs(r.toff) + (double)chunk) < 0x1p29));
 }
 
 // the f64 libm of the reference step (pll.cpp:39, :49-50), out of line: only the rare fallbacks
@@ -937,33 +951,45 @@ __device__ __noinline__ void pll_sincos_ref(float t, double* s, double* c) { sin
 
 // One step of pll.cpp:36-50. CHECKED: every result the fast path cannot prove is recomputed
 // with the f64 libm exactly as the reference (used for chunk redo and short tails).
-template <bool CHECKED>
-__device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float Kp, float Ki, double w,
+template <bool CHECKED, bool TAB>
+__device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float Kp, float Ki, double w, double wt,
                                          float& t_out, PllProof& pf) {
-    const float eI = x * r.fbI;                               // pll.cpp:36
-    const float eQ = x * (-r.fbQ);                            // pll.cpp:37
+    // pll.cpp:36-37 in the reduced frame, as one packed multiply: x * (fbI, -fbQ)
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v fb = {r.fbI, -r.fbQ};
+    const f2v ee = x * fb;
+    const float eI0 = ee.x, eQ0 = ee.y;
     const double base = pllm::base_angle(pllm::lo_word(rx), r.q, r.b, r.mr);
-    const pllm::Phase2 p = pllm::phase_detect2(eI, eQ, r.c, r.s, rx, base);
+    const pllm::Phase2 p = pllm::phase_detect_r(eI0, eQ0, r.c, r.s, rx, base);
     float e = p.ef;
-    if (CHECKED && !((__builtin_fabs(p.e) < pllm::PI - 0x1p-30) && p.split == 0u))
-        e = pll_atan2_ref(eQ, eI);                            // pll.cpp:39
+    if (CHECKED && !((__builtin_fabs(p.e) < pllm::PI - 0x1p-30) && p.split == 0u)) {
+        float a = eI0, b = -eQ0;                              // eI - i eQ = i^q (eI0 - i eQ0)
+        pllm::rot_q(r.q, a, b);
+        e = pll_atan2_ref(-b, a);                             // pll.cpp:39
+    }
     r.integ = r.integ + Ki * e;                               // pll.cpp:41
     r.ph = r.ph + Kp * e + r.integ;                           // pll.cpp:42
-    r.toff += 1.0;                                            // pll.cpp:46
-    const float t = (float)(w * r.toff + (double)r.ph);       // pll.cpp:47
-    const pllm::SinCos2 sc = pllm::sincos2_f32(t);
-    r.c = sc.c;
-    r.s = sc.s;
+    float t;
+    if (TAB) {                                                // wt = w * trigOffset, tabulated
+        t = (float)(wt + (double)r.ph);                       // pll.cpp:47
+    } else {
+        r.toff += 1.0;                                        // pll.cpp:46
+        t = (float)(w * r.toff + (double)r.ph);               // pll.cpp:47
+    }
+    const pllm::SinCosR sc = pllm::sincos_r(t);
+    r.c = sc.cr;
+    r.s = sc.sr;
     r.mr = sc.mr;
     r.q = sc.q;
     r.b = sc.b;
-    r.fbI = (float)sc.c;                                      // pll.cpp:49
-    r.fbQ = (float)sc.s;                                      // pll.cpp:50
+    r.fbI = (float)sc.cr;                                     // pll.cpp:49-50, reduced frame
+    r.fbQ = (float)sc.sr;
     if (CHECKED) {
         const bool in_range = __builtin_fabs((double)t) < pllm::T_MAX;
         if (!(in_range && sc.tie > 128u)) {
             double sv, cv;
             pll_sincos_ref(t, &sv, &cv);
+            pllm::rot_q(0u - r.q, cv, sv);                    // into the reduced frame, exactly
             r.fbI = (float)cv;
             r.fbQ = (float)sv;
             r.c = cv;
@@ -987,19 +1013,18 @@ constexpr int PLL_NBUF = SDR_PLL_NBUF;   // register buffers of inputs (prefetch
 // VEC: x / rx rows and the t buffer are 16-byte aligned with strides that are multiples of 4
 // (x, t) and 2 (rx), so a chunk's inputs are prefetched with 16-byte loads one chunk ahead and
 // the 16 phases are stored with 16-byte stores -- the unrolled chunk itself touches no memory.
-template <bool VEC>
-__global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) {
-    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ch >= nch) return;
-    const PllJob& jb = jobs.j[blockIdx.y];
+// One lane per channel runs the n serial steps of one PllJob.
+// TAB: every lane of the wave has the same trigOffset (a context's channels advance together), so
+// w * trigOffset of every step comes from a table the wave builds in LDS up front (pll.cpp:46-47
+// evaluated once per step index instead of once per channel and step).
+template <bool VEC, bool TAB>
+__device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const double* __restrict__ wtab) {
     const float* __restrict__ in = jb.in;
     const size_t in_stride = jb.in_stride, t_stride = jb.t_stride, out_stride = jb.out_stride;
     float* __restrict__ tbuf = jb.tbuf;
     float* __restrict__ out = jb.out;
     sdr_pll_state* __restrict__ st = jb.st;
     const float freq = jb.freq, Fs = jb.Fs, normBandwidth = jb.bw;
-    // the serial PLL bounds every block-step: let its waves win issue arbitration on shared SIMDs
-    __builtin_amdgcn_s_setprio(3);
     const float Cp = 2.666;
     const float Ci = 3.555;
     const float Kp = normBandwidth * Cp;
@@ -1049,15 +1074,25 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) 
 #pragma unroll
         for (int u = 0; u < NB; u++) {
             const int i0 = (c0 + u) * C;
+            double wv[C];
+            if (TAB) {
+#pragma unroll
+                for (int k = 0; k < C / 2; k++) {
+                    const double2 v = reinterpret_cast<const double2*>(wtab + i0)[k];
+                    wv[2 * k] = v.x; wv[2 * k + 1] = v.y;
+                }
+            }
             const PllRegs snap = r;
             PllProof pf;
             float tv[C];
 #pragma unroll
-            for (int j = 0; j < C; j++) pll_step<false>(r, xb[u][j], rb[u][j], Kp, Ki, w, tv[j], pf);
-            if (!pll_chunk_ok(pf, r, w, C)) {
+            for (int j = 0; j < C; j++)
+                pll_step<false, TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
+            if (!pll_chunk_ok<TAB>(pf, r, w, C)) {
                 r = snap;
 #pragma unroll
-                for (int j = 0; j < C; j++) pll_step<true>(r, xb[u][j], rb[u][j], Kp, Ki, w, tv[j], pf);
+                for (int j = 0; j < C; j++)
+                    pll_step<true, TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
             }
             if (VEC) {
 #pragma unroll
@@ -1073,14 +1108,46 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch) 
     }
     {
         PllProof pf;
-        for (int i = nmain * C; i < n; i++) pll_step<true>(r, x[i], rxp[i], Kp, Ki, w, tb[i], pf);
+        for (int i = nmain * C; i < n; i++)
+            pll_step<true, TAB>(r, x[i], rxp[i], Kp, Ki, w, TAB ? wtab[i] : 0.0, tb[i], pf);
     }
-    // every field but lastCarrier (k_nco_out's)
+    if (TAB) r.toff = s0.trigOffset + (double)n;               // pll.cpp:46, n times (exact)
+    // every field but lastCarrier (k_nco_out's); the feedback back in the frame of t
+    pllm::rot_q(r.q, r.fbI, r.fbQ);
     st[ch].feedbackI = r.fbI;
     st[ch].feedbackQ = r.fbQ;
     st[ch].integrator = r.integ;
     st[ch].phaseEst = r.ph;
     st[ch].trigOffset = r.toff;
+}
+
+// VEC: x / rx rows and the t buffer are 16-byte aligned with strides that are multiples of 4
+// (x, t) and 2 (rx), so a chunk's inputs are prefetched with 16-byte loads and the 16 phases are
+// stored with 16-byte stores -- the unrolled chunk itself touches no memory.
+// Dynamic LDS: n doubles when the launch allows the trigArg table (launch_plls), else none.
+template <bool VEC>
+__global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, int tab_ok) {
+    extern __shared__ double wtab[];
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;   // lane 0 always holds a channel
+    const bool active = ch < nch;
+    const PllJob& jb = jobs.j[blockIdx.y];
+    // the serial PLL bounds every block-step: let its waves win issue arbitration on shared SIMDs
+    __builtin_amdgcn_s_setprio(3);
+    const double toff0 = active ? jb.st[ch].trigOffset : 0.0;
+    const double w = 2 * 3.14159265358979323846 * (jb.freq / jb.Fs);
+    // one wave per workgroup: the table is valid when all channels of the wave share trigOffset
+    // and every w * trigOffset of the launch stays below 2^29 (so |t| < 2^30 whenever
+    // |phaseEst| < 2^28). All 64 lanes build it, then the lanes without a channel leave.
+    const double toff_l0 = __shfl(toff0, 0);
+    const bool tab = tab_ok && __all(!active || toff0 == toff_l0) &&
+                     __builtin_fabs(w) * (__builtin_fabs(toff_l0) + (double)n + 1.0) < 0x1p29;
+    if (tab) {
+        for (int k = threadIdx.x; k < n; k += 64) wtab[k] = w * (toff_l0 + (double)(k + 1));   // pll.cpp:46-47
+        __syncthreads();
+    }
+    if (!active) return;
+    if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
+    else pll_run<VEC, false>(jb, n, ch, nullptr);
 }
 
 // pll_rx of a PLL input with no fused producer (the batched sdr_fmpll primitive)
@@ -1460,6 +1527,15 @@ bool pll_libm_env() {
     return v;
 }
 
+// SDR_PLL_TAB=0: per-lane trigArg offsets (A/B of the LDS table)
+bool pll_notab_env() {
+    static const bool v = [] {
+        const char* e = std::getenv("SDR_PLL_TAB");
+        return e && std::strcmp(e, "0") == 0;
+    }();
+    return v;
+}
+
 int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
     if (n > 0) {
         hipLaunchKernelGGL(k_nco_out, dim3(cdiv(n, BLK), nch, njobs), dim3(BLK), 0, s, jobs, n);
@@ -1477,12 +1553,16 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
               (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
               (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0);
     }
+    // LDS table of w * trigOffset (k_pll): n doubles, 16-byte rows
+    const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
+    const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
+    const size_t lds = tab_ok ? tab_bytes : 0;
     if (libm || pll_libm_env()) {
         hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, jobs, n, nch);
     } else if (vec) {
-        hipLaunchKernelGGL(k_pll<true>, g, b, 0, s, jobs, n, nch);
+        hipLaunchKernelGGL(k_pll<true>, g, b, lds, s, jobs, n, nch, tab_ok);
     } else {
-        hipLaunchKernelGGL(k_pll<false>, g, b, 0, s, jobs, n, nch);
+        hipLaunchKernelGGL(k_pll<false>, g, b, lds, s, jobs, n, nch, tab_ok);
     }
     LAUNCH_CHECK();
     return with_nco ? launch_nco(jobs, njobs, n, nch, s) : SDR_OK;

@@ -1,13 +1,21 @@
-# A/B of library variants (build/variants/<name>.so from tools/build_variant.sh; "default" = the
-# in-tree libsdr_amd.so) on the full bench, interleaved REPS times.  VARIANTS="default nb3" REPS=2
+# A/B of library variants on the full bench, interleaved REPS times. A variant is
+#   default          the in-tree libsdr_amd.so
+#   <name>           build/variants/<name>.so (tools/build_variant.sh)
+#   <name>@VAR=val   either of the above with an environment setting (e.g. default@SDR_PLL_TAB=0)
+#   VARIANTS="default nb3 default@SDR_PLL_TAB=0" REPS=2 bash tools/gpu/ab_bench.sh
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-abb}
 mkdir -p $O
+i=0
 for rep in $(seq ${REPS:-2}); do
 for v in ${VARIANTS:-default}; do
-  if [ "$v" = default ]; then L=""; else L="build/variants/$v.so"; fi
-  env SDR_AMD_LIB=$L timeout -k 10 200 python bench.py --no-cpu-baseline --no-isolated ${BENCH_ARGS:-} > $O/b_$v.json 2> $O/b_$v.err; rc=$?
-  echo "$v $(python3 -c "import json,sys; d=json.load(open('$O/b_$v.json')); print(d['value'], d['ms_per_step'])")"; [ $rc -eq 0 ] || exit $rc
+  i=$((i+1))
+  lib=${v%%@*}; envs=""
+  [ "$lib" != "$v" ] && envs=${v#*@}
+  if [ "$lib" = default ]; then L=""; else L="build/variants/$lib.so"; fi
+  env SDR_AMD_LIB=$L $envs timeout -k 10 200 python bench.py --no-cpu-baseline --no-isolated ${BENCH_ARGS:-} > $O/b_$i.json 2> $O/b_$i.err; rc=$?
+  [ $rc -eq 0 ] || { tail -5 $O/b_$i.err; exit $rc; }
+  echo "$v $(python3 -c "import json; d=json.load(open('$O/b_$i.json')); print(d['value'], d['ms_per_step'])")"
 done
 done

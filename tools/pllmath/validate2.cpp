@@ -135,5 +135,82 @@ int main(int argc, char** argv) {
     }
     std::printf("pll2:   steps %ld diverged %ld fallbacks e %ld (%.2e) sincos %ld (%.2e)\n", steps, diff, fb_e,
                 (double)fb_e / steps, fb_sc, (double)fb_sc / steps);
+
+    // 4) reduced-frame trajectories (k_pll): feedback carried as RN(cos r), RN(sin r) and q
+    long rsteps = 0, rdiff = 0, rfb_e = 0, rfb_sc = 0;
+    for (int sig = 0; sig < 8; sig++) {
+        const float freq = (sig & 1) ? 114e3f : 19e3f, Fs = 240000.0f;
+        const float bw = (sig & 1) ? 0.001f : 0.01f;
+        const float Cp = 2.666, Ci = 3.555;
+        const float Kp = bw * Cp, Ki = bw * bw * Ci;
+        const double w = 2 * 3.14159265358979323846 * (freq / Fs);
+        double toff = sig >= 4 ? 3.0e6 : 0.0, rtoff = toff;
+        const float t0 = (float)(w * toff);
+        float rfbI = (float)std::cos((double)t0), rfbQ = (float)std::sin((double)t0), rinteg = 0, rph = 0;
+        // kernel state: pll_load
+        float integ = 0, ph = 0;
+        pllm::SinCosR sc = pllm::sincos_r(t0);
+        float fI0 = (float)sc.cr, fQ0 = (float)sc.sr;
+        {
+            float a = fI0, b = fQ0;
+            pllm::rot_q(sc.q, a, b);
+            if (a != rfbI || b != rfbQ) std::printf("load: inconsistent state\n");
+        }
+        double cr = sc.cr, sr = sc.sr, mr = sc.mr;
+        uint32_t q = sc.q, bsg = sc.b;
+        const long n = N / 8;
+        for (long i = 0; i < n; i++) {
+            const float xin = (float)(0.1 * std::cos(2 * M_PI * (freq + 3.0 * sig) / Fs * i + sig) +
+                                      0.01 * (U(rng) - 0.5));
+            {
+                const float eI = xin * rfbI, eQ = xin * (-rfbQ);
+                const float e = std::atan2((double)eQ, (double)eI);
+                rinteg = rinteg + Ki * e;
+                rph = rph + Kp * e + rinteg;
+                rtoff += 1.0;
+                const float t = 2 * 3.14159265358979323846 * (freq / Fs) * rtoff + rph;
+                rfbI = std::cos((double)t);
+                rfbQ = std::sin((double)t);
+            }
+            {
+                const float eI0 = xin * fI0, eQ0 = xin * (-fQ0);
+                const double rx = pllm::pll_rx(xin);
+                const double base = pllm::base_angle(pllm::lo_word(rx), q, bsg, mr);
+                const pllm::Phase2 p = pllm::phase_detect_r(eI0, eQ0, cr, sr, rx, base);
+                float e = p.ef;
+                if (!(std::fabs(p.e) < pllm::PI - 0x1p-30 && p.split == 0u)) {
+                    float a = eI0, b = -eQ0;
+                    pllm::rot_q(q, a, b);
+                    e = (float)std::atan2((double)(-b), (double)a);
+                    rfb_e++;
+                }
+                integ = integ + Ki * e;
+                ph = ph + Kp * e + integ;
+                toff += 1.0;
+                const float t = (float)(w * toff + (double)ph);
+                sc = pllm::sincos_r(t);
+                cr = sc.cr; sr = sc.sr; mr = sc.mr; q = sc.q; bsg = sc.b;
+                fI0 = (float)cr; fQ0 = (float)sr;
+                if (!(sc.tie > 128u)) {
+                    double cv = std::cos((double)t), sv = std::sin((double)t);
+                    pllm::rot_q(0u - q, cv, sv);
+                    cr = cv; sr = sv;
+                    fI0 = (float)cr; fQ0 = (float)sr;
+                    rfb_sc++;
+                }
+            }
+            rsteps++;
+            float fbI = fI0, fbQ = fQ0;
+            pllm::rot_q(q, fbI, fbQ);
+            if (fbI != rfbI || fbQ != rfbQ || ph != rph || integ != rinteg) {
+                if (rdiff < 5) std::printf("reduced-frame PLL diverged sig %d step %ld\n", sig, i);
+                rdiff++;
+                break;
+            }
+        }
+    }
+    std::printf("pllR:   steps %ld diverged %ld fallbacks e %ld (%.2e) sincos %ld (%.2e)\n", rsteps, rdiff, rfb_e,
+                (double)rfb_e / rsteps, rfb_sc, (double)rfb_sc / rsteps);
+    diff += rdiff;
     return (sc_mis || pd_mis || diff) ? 1 : 0;
 }
