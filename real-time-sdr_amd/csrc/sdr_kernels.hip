@@ -780,13 +780,114 @@ __global__ __launch_bounds__(BLK) void k_fir(const float* __restrict__ x, size_t
 }
 
 // ------------------------------------------------------------------------------------------
+// The IF-rate 101-tap FIRs without decimation (filter.cpp:106-121 with D = 1: pilot/band BPFs
+// stereo.cpp:74,80, RDS BPF rds.cpp:105, squared-RDS BPF :116, RRC :133), register-blocked:
+// each thread computes FRB_R consecutive outputs from a window of FRB_R + 100 samples read once
+// from LDS (16-byte reads), the taps are wave-uniform scalar loads, and every output still sums
+// h[k] * x[n-k] in ascending k as an f32 product then an f32 add (no contraction). NT = 2: two tap
+// sets over one window (the stereo pilot and band filters).
+// ------------------------------------------------------------------------------------------
+constexpr int FRB_T = 101;                 // taps (rf_taps, project.cpp:61)
+constexpr int FRB_R = 8;                   // outputs per thread
+constexpr int FRB_TILE = BLK * FRB_R;      // outputs per workgroup
+constexpr int FRB_W = FRB_TILE + FRB_T - 1 + 3;   // staged samples (+3: whole 16-byte reads)
+
+template <int NT, bool SQUARE>
+__global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, size_t x_stride,
+                                                const float* __restrict__ hist, size_t hist_stride,
+                                                const float* __restrict__ h0, const float* __restrict__ h1, int ny,
+                                                float* __restrict__ y0, float* __restrict__ y1, size_t y_stride,
+                                                double* __restrict__ rx0, size_t rx_stride) {
+    constexpr int T = FRB_T, R = FRB_R;
+    __shared__ __attribute__((aligned(16))) float sx[(FRB_W + 3) & ~3];
+    const int ch = blockIdx.y, tid = threadIdx.x;
+    const int n0 = blockIdx.x * FRB_TILE;
+    const int m0 = n0 - (T - 1);
+    const int W = min(FRB_TILE, ny - n0) + T - 1;
+    {
+        // all loads of the tile in flight at once, then the LDS writes
+        const float* xc = x + (size_t)ch * x_stride;
+        const float* hc = hist + (size_t)ch * hist_stride;
+        constexpr int NL = (FRB_TILE + FRB_T - 1 + BLK - 1) / BLK;
+        float v[NL];
+#pragma unroll
+        for (int u = 0; u < NL; u++) {
+            const int i = tid + u * BLK, m = m0 + i;
+            v[u] = (i < W) ? (m < 0 ? hc : xc)[m] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < NL; u++) {
+            const int i = tid + u * BLK;
+            if (i < W) sx[i] = SQUARE ? v[u] * v[u] : v[u];       // rds.cpp:111-113
+        }
+    }
+    __syncthreads();
+    const int nb = n0 + tid * R;
+    if (nb >= ny) return;
+    // w[i] = x[nb - (T-1) + i]; output nb + j at tap k reads w[j + T-1 - k] (samples past the
+    // staged window only feed outputs >= ny, which are not stored)
+    float w[R + T - 1 + 3];
+#pragma unroll
+    for (int i = 0; i < (R + T - 1 + 3) / 4; i++) {
+        const float4 v = reinterpret_cast<const float4*>(sx + tid * R)[i];
+        w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+    float a0[R], a1[R];
+#pragma unroll
+    for (int j = 0; j < R; j++) { a0[j] = 0.0f; a1[j] = 0.0f; }
+#pragma unroll
+    for (int k = 0; k < T; k++) {
+        const float c0 = h0[k];
+        const float c1 = (NT == 2) ? h1[k] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            const float v = w[j + T - 1 - k];
+            a0[j] = a0[j] + c0 * v;                               // filter.cpp:115
+            if (NT == 2) a1[j] = a1[j] + c1 * v;
+            // keep the MACs scalar: packed f32 ops run at half rate (tools/microbench/valu_rate.hip)
+            // and pairing neighbouring outputs costs register realignment and occupancy
+            if (NT == 1 && (j & 1) == 0) asm volatile("" : "+v"(a0[j]));
+        }
+    }
+    float* o0 = y0 + (size_t)ch * y_stride + nb;
+    float* o1 = (NT == 2) ? y1 + (size_t)ch * y_stride + nb : nullptr;
+    if (nb + R <= ny) {
+#pragma unroll
+        for (int j = 0; j < R; j += 4) {
+            reinterpret_cast<float4*>(o0 + j)[0] = make_float4(a0[j], a0[j + 1], a0[j + 2], a0[j + 3]);
+            if (NT == 2) reinterpret_cast<float4*>(o1 + j)[0] = make_float4(a1[j], a1[j + 1], a1[j + 2], a1[j + 3]);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            if (nb + j < ny) {
+                o0[j] = a0[j];
+                if (NT == 2) o1[j] = a1[j];
+            }
+        }
+    }
+    if (rx0) {                                                    // y0 feeds a PLL: its reciprocal
+        double* r = rx0 + (size_t)ch * rx_stride + nb;
+        if (nb + R <= ny) {
+#pragma unroll
+            for (int j = 0; j < R; j += 2)
+                reinterpret_cast<double2*>(r + j)[0] = make_double2(pllm::pll_rx(a0[j]), pllm::pll_rx(a0[j + 1]));
+        } else {
+#pragma unroll
+            for (int j = 0; j < R; j++)
+                if (nb + j < ny) r[j] = pllm::pll_rx(a0[j]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Rational resampler, filter.cpp:123-147. Output n: phase = nD mod U, q = (nD - phase)/U,
 // y[n] = sum_j hp[phase][j] * x[q - j] (j ascending == k ascending), hp = polyphase taps,
 // cnt[phase] = number of taps of that phase. The phase restarts every block (the reference
 // recomputes it from n, :131). OUT: 0 -> f32 y, 1 -> int16(16384*y) (mono.cpp:40-42),
 // 2 -> stereo L/R int16 from two inputs a (mono) and b (stereo) (stereo.cpp:100-107).
 // ------------------------------------------------------------------------------------------
-template <int OUT>
+template <int OUT, int NTAP = 0>   // NTAP > 0: U == 1 with NTAP taps (uniform taps, unrolled sums)
 __global__ __launch_bounds__(BLK) void k_resample(const float* __restrict__ xa, const float* __restrict__ ha,
                                                   size_t xa_stride, size_t ha_stride,
                                                   const float* __restrict__ xb, const float* __restrict__ hb,
@@ -803,35 +904,44 @@ __global__ __launch_bounds__(BLK) void k_resample(const float* __restrict__ xa, 
     const int W = qhi - qlo + 1;
     const int Wp = (W + 3) & ~3;
     float* sb = sa + Wp;
-    {
-        const float* xc = xa + (size_t)ch * xa_stride;
-        const float* hc = ha + (size_t)ch * ha_stride;
-        for (int i = tid; i < W; i += BLK) {
-            const int m = qlo + i;
-            sa[i] = (m < 0) ? (m >= hist_lo ? hc[m] : 0.0f) : xc[m];
+    // staging: 4 loads per thread in flight per round
+    auto stage = [&](float* dst, const float* xc, const float* hc) {
+        for (int i0 = tid; i0 < W; i0 += 4 * BLK) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * BLK, m = qlo + i;
+                v[u] = (i < W && m >= hist_lo) ? (m < 0 ? hc : xc)[m] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (i0 + u * BLK < W) dst[i0 + u * BLK] = v[u];
         }
-    }
-    if (OUT == 2) {
-        const float* xc = xb + (size_t)ch * xb_stride;
-        const float* hc = hb + (size_t)ch * hb_stride;
-        for (int i = tid; i < W; i += BLK) {
-            const int m = qlo + i;
-            sb[i] = (m < 0) ? (m >= hist_lo ? hc[m] : 0.0f) : xc[m];
-        }
-    }
+    };
+    stage(sa, xa + (size_t)ch * xa_stride, ha + (size_t)ch * ha_stride);
+    if (OUT == 2) stage(sb, xb + (size_t)ch * xb_stride, hb + (size_t)ch * hb_stride);
     __syncthreads();
     for (int n = n0 + tid; n < n1; n += BLK) {
         const long long nd = (long long)n * D;
-        const int ph = (int)(nd % U);
-        const int q = (int)(nd / U);
+        const int ph = NTAP > 0 ? 0 : (int)(nd % U);
+        const int q = NTAP > 0 ? (int)nd : (int)(nd / U);
         const float* hr = hp + (size_t)ph * L;
-        const int c = cnt[ph];
         const int base = q - qlo;
         float a = 0.0f, b = 0.0f;
-        for (int j = 0; j < c; j++) {
-            const float hj = hr[j];
-            a = a + hj * sa[base - j];
-            if (OUT == 2) b = b + hj * sb[base - j];
+        if (NTAP > 0) {                 // one polyphase row (U = 1): wave-uniform scalar taps
+#pragma unroll 8
+            for (int j = 0; j < NTAP; j++) {
+                const float hj = hp[j];
+                a = a + hj * sa[base - j];
+                if (OUT == 2) b = b + hj * sb[base - j];
+            }
+        } else {
+            const int c = cnt[ph];
+            for (int j = 0; j < c; j++) {
+                const float hj = hr[j];
+                a = a + hj * sa[base - j];
+                if (OUT == 2) b = b + hj * sb[base - j];
+            }
         }
         if (OUT == 0) {
             static_cast<float*>(y)[(size_t)ch * y_stride + n] = a;
@@ -843,6 +953,128 @@ __global__ __launch_bounds__(BLK) void k_resample(const float* __restrict__ xa, 
             o[1] = cvt_i16_x86(16384 * (a - b));   // right = 16384*(m - s)
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// The RDS 247/640 resampler (rds.cpp:130 -> filter.cpp:123-147) with lanes = channels: a
+// workgroup takes 64 channels x RLC_TN outputs. Every output has its own polyphase row, shared by
+// all 64 channels, so the rows of the tile are staged once in LDS and read as broadcasts, while
+// each lane reads its own channel's samples from an odd-strided LDS tile (no bank conflicts).
+// ptq[n] = (q << 8) | phase with phase = nD mod U, q = nD / U (host table; U < 256). Sums stay
+// in ascending j (= ascending k of the reference) as f32 product then f32 add.
+// ------------------------------------------------------------------------------------------
+constexpr int RLC_TN = 32;     // outputs per workgroup (8 per wave)
+constexpr int RLC_XL = 3;      // staged samples per lane and row: 64 * 3 >= the q span + look-back
+constexpr int RLC_HL = 2;      // staged taps per lane and polyphase row: 64 * 2 >= L4
+
+template <int NTAP>   // > 0: every polyphase row has exactly NTAP taps (fully unrolled sums)
+__global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x, size_t x_stride, int hist_lo,
+                                                     const float* __restrict__ hp, const int* __restrict__ cnt,
+                                                     int L, const int* __restrict__ ptq, int ny, int nch,
+                                                     float* __restrict__ y, size_t y_stride) {
+    extern __shared__ float4 smem4[];
+    float* smem = reinterpret_cast<float*>(smem4);
+    constexpr int PW = RLC_TN / (BLK / 64);                  // outputs per wave
+    const int c0 = blockIdx.y * 64, n0 = blockIdx.x * RLC_TN;
+    const int nn = min(RLC_TN, ny - n0);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int qlo = (ptq[n0] >> 8) - (L - 1);
+    const int W = (ptq[n0 + nn - 1] >> 8) - qlo + 1;
+    const int SW = W | 1;
+    const int L4 = (L + 3) & ~3;
+    float* sx = smem;                                        // [64][SW]
+    float* sh = smem + ((64 * SW + 3) & ~3);                 // [RLC_TN][L4]
+    // staging with every load of a wave in flight before its LDS writes: rows c = wave + 4u of the
+    // x tile (lanes along the row, RLC_XL loads per row), then the polyphase rows of the outputs
+    {
+        constexpr int NR = 64 / (BLK / 64);
+        float v[NR][RLC_XL];
+#pragma unroll
+        for (int u = 0; u < NR; u++) {
+            const int ch = min(c0 + wave + u * (BLK / 64), nch - 1);
+            const float* xc = x + (size_t)ch * x_stride;
+#pragma unroll
+            for (int k = 0; k < RLC_XL; k++) {
+                const int i = lane + 64 * k, m = qlo + i;
+                v[u][k] = (i < W && m >= hist_lo) ? xc[m] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NR; u++) {
+            const int c = wave + u * (BLK / 64);
+#pragma unroll
+            for (int k = 0; k < RLC_XL; k++) {
+                const int i = lane + 64 * k;
+                if (i < W) sx[c * SW + i] = v[u][k];
+            }
+        }
+        float hv[PW][RLC_HL];
+#pragma unroll
+        for (int o8 = 0; o8 < PW; o8++) {
+            const int o = min(wave * PW + o8, nn - 1);
+            const int ph = ptq[n0 + o] & 255;
+            const int cn = cnt[ph];
+#pragma unroll
+            for (int k = 0; k < RLC_HL; k++) {
+                const int j = lane + 64 * k;
+                hv[o8][k] = (j < cn) ? hp[(size_t)ph * L + j] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int o8 = 0; o8 < PW; o8++) {
+            const int o = wave * PW + o8;
+#pragma unroll
+            for (int k = 0; k < RLC_HL; k++) {
+                const int j = lane + 64 * k;
+                if (o < nn && j < L4) sh[o * L4 + j] = hv[o8][k];
+            }
+        }
+    }
+    __syncthreads();
+    const int ch = c0 + lane;
+    float out[PW];
+#pragma unroll
+    for (int o8 = 0; o8 < PW; o8++) {
+        const int o = wave * PW + o8;
+        float acc = 0.0f;
+        if (o < nn) {
+            const int e = ptq[n0 + o];
+            const int cn = cnt[e & 255];
+            const float* xr = sx + lane * SW + ((e >> 8) - qlo);  // x[q - j] = xr[-j]
+            const float* hr = sh + o * L4;
+            if (NTAP > 0) {
+#pragma unroll
+                for (int j = 0; j < NTAP; j++) acc = acc + hr[j] * xr[-j];
+            } else {
+            int j = 0;
+            for (; j + 4 <= cn; j += 4) {
+                const float4 h4 = *reinterpret_cast<const float4*>(hr + j);
+                acc = acc + h4.x * xr[-j];
+                acc = acc + h4.y * xr[-j - 1];
+                acc = acc + h4.z * xr[-j - 2];
+                acc = acc + h4.w * xr[-j - 3];
+            }
+            for (; j < cn; j++) acc = acc + hr[j] * xr[-j];
+            }
+        }
+        out[o8] = acc;
+    }
+    if (ch < nch) {
+        float* yo = y + (size_t)ch * y_stride + n0 + wave * PW;
+        const int m = min(PW, nn - wave * PW);
+#pragma unroll
+        for (int o8 = 0; o8 < PW; o8++)
+            if (o8 < m) yo[o8] = out[o8];
+    }
+}
+
+int resample_lc_span(int L, int U, int D) {   // samples a tile reads: q span + look-back
+    return (int)(((long long)(RLC_TN - 1) * D + U - 1) / U) + 1 + L;
+}
+
+size_t resample_lc_lds_bytes(int L, int U, int D) {
+    const int W = resample_lc_span(L, U, D);
+    return (size_t)((((64 * (W | 1)) + 3) & ~3) + RLC_TN * ((L + 3) & ~3)) * sizeof(float);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1604,6 +1836,9 @@ struct sdr_ctx {
     // plain per-block buffers
     float *pilot = nullptr, *band = nullptr, *gpilot = nullptr, *carrier = nullptr, *ipll = nullptr,
           *rds_clean = nullptr, *t_st = nullptr, *t_rds = nullptr;
+    int* rds_ptq = nullptr;                             // RDS resampler (q << 8 | phase) per output
+    bool rdsbb_all101 = false;                          // every RDS polyphase row has 101 taps
+    bool audio_u1_101 = false;                          // audio resampler U == 1 with 101 taps
     double *rx_st = nullptr, *rx_rds = nullptr;         // PLL input reciprocals (pll_math.h pll_rx),
                                                         // [2 parities][nch][plain_stride], from the FIRs
     size_t plain_stride = 0, pll_stride = 0, clean_stride = 0;
@@ -1847,6 +2082,8 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     TRY(upload(c, &c->audio_cnt, pa.cnt));
     TRY(upload(c, &c->rdsbb_pp, pr.table));
     TRY(upload(c, &c->rdsbb_cnt, pr.cnt));
+    c->rdsbb_all101 = std::all_of(pr.cnt.begin(), pr.cnt.end(), [](int k) { return k == 101; });
+    c->audio_u1_101 = in.audio_upsample == 1 && pa.cnt.size() == 1 && pa.cnt[0] == 101;
     // ---- extended streams ----
     c->fm_stride = round_up((size_t)HIST + in.block_if, 64);
     c->rf_stride = round_up((size_t)HIST + in.n_rds, 64);
@@ -1868,6 +2105,14 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     TRY(dalloc(c, &c->gpilot, 2 * c->plain_par));
     TRY(dalloc(c, &c->t_st, 2 * c->plain_par));
     TRY(dalloc(c, &c->t_rds, 2 * c->plain_par));
+    {
+        std::vector<int> ptq(std::max(in.n_rds, 1));
+        for (int k = 0; k < in.n_rds; k++) {                // rds.cpp:130: U = 247, D = 640
+            const long long nd = (long long)k * 640;
+            ptq[k] = (int)((nd / 247) << 8) | (int)(nd % 247);
+        }
+        TRY(upload(c, &c->rds_ptq, ptq));
+    }
     TRY(dalloc(c, &c->rx_st, 2 * c->plain_par));
     TRY(dalloc(c, &c->rx_rds, 2 * c->plain_par));
     TRY(dalloc(c, &c->carrier, 2 * c->pll_par));
@@ -2003,7 +2248,8 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
     dim3 grid(cdiv(in.n_audio, tile), c->nch);
     const size_t lds = resample_lds_bytes(c->audio_L, in.audio_upsample, in.audio_decim, tile, 1);
     const float* fm = c->fm_cur();
-    hipLaunchKernelGGL(k_resample<1>, grid, dim3(BLK), lds, S(stream), fm, fm, c->fm_stride, c->fm_stride,
+    auto km = c->audio_u1_101 ? k_resample<1, 101> : k_resample<1, 0>;
+    hipLaunchKernelGGL(km, grid, dim3(BLK), lds, S(stream), fm, fm, c->fm_stride, c->fm_stride,
                        nullptr, nullptr, (size_t)0, (size_t)0, c->audio_pp, c->audio_cnt, c->audio_L,
                        in.audio_upsample, in.audio_decim, in.n_audio, tile, -HIST, (void*)audio, audio_stride);
     LAUNCH_CHECK();
@@ -2022,10 +2268,11 @@ int sdr_stereo_pre(sdr_ctx* c, void* stream) {
     const int n = in.block_if, T = c->ntaps;
     const float* fm = c->fm_cur();
     // pilot BPF (stereo.cpp:74) + band BPF (:80) from one staged window of fm_demod
-    dim3 gf(cdiv(n, FIR_TILE), c->nch);
-    hipLaunchKernelGGL((k_fir<2, false>), gf, dim3(BLK), fir_lds_bytes(T, 2, FIR_TILE, 1), S(stream), fm,
-                       c->fm_stride, fm, c->fm_stride, c->pilot_h, c->stereo_h, T, 1, n, FIR_TILE, c->plain(c->pilot),
-                       c->plain(c->band), c->plain_stride, c->rxbuf(c->rx_st), c->plain_stride);
+    if (T != FRB_T) return fail(SDR_E_INVALID, "stereo_pre: %d taps", T);
+    dim3 gf(cdiv(n, FRB_TILE), c->nch);
+    hipLaunchKernelGGL((k_fir_rb<2, false>), gf, dim3(BLK), 0, S(stream), fm, c->fm_stride, fm, c->fm_stride,
+                       c->pilot_h, c->stereo_h, n, c->plain(c->pilot), c->plain(c->band), c->plain_stride,
+                       c->rxbuf(c->rx_st), c->plain_stride);
     LAUNCH_CHECK();
     c->st_pre_done = c->block;
     return SDR_OK;
@@ -2069,7 +2316,8 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
     const int tile = 512;
     dim3 gr(cdiv(in.n_audio, tile), c->nch);
     const size_t lds = resample_lds_bytes(c->audio_L, in.audio_upsample, in.audio_decim, tile, 2);
-    hipLaunchKernelGGL(k_resample<2>, gr, dim3(BLK), lds, s, fm - 50, fm - 50, c->fm_stride, c->fm_stride, sdc, sdc,
+    auto ks = c->audio_u1_101 ? k_resample<2, 101> : k_resample<2, 0>;
+    hipLaunchKernelGGL(ks, gr, dim3(BLK), lds, s, fm - 50, fm - 50, c->fm_stride, c->fm_stride, sdc, sdc,
                        c->fm_stride, c->fm_stride, c->audio_pp, c->audio_cnt, c->audio_L, in.audio_upsample,
                        in.audio_decim, in.n_audio, tile, -(HIST - 50), (void*)lr, lr_stride);
     LAUNCH_CHECK();
@@ -2094,18 +2342,19 @@ int sdr_rds_pre(sdr_ctx* c, void* stream) {
     const int n = in.block_if, T = c->ntaps, p = c->parity;
     const float* fm = c->fm_cur();
     float* rband = c->rband + p * c->fm_par;
-    dim3 gf(cdiv(n, FIR_TILE), c->nch);
+    if (T != FRB_T) return fail(SDR_E_INVALID, "rds_pre: %d taps", T);
+    dim3 gf(cdiv(n, FRB_TILE), c->nch);
     // RDS band BPF (rds.cpp:105) into the extended rds_band stream
     hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rband, c->rband + (p ^ 1) * c->fm_par,
                        c->fm_stride, n);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL((k_fir<1, false>), gf, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, fm, c->fm_stride, fm,
-                       c->fm_stride, c->rds_h, nullptr, T, 1, n, FIR_TILE, rband, nullptr, c->fm_stride, nullptr, 0);
+    hipLaunchKernelGGL((k_fir_rb<1, false>), gf, dim3(BLK), 0, s, fm, c->fm_stride, fm, c->fm_stride, c->rds_h,
+                       nullptr, n, rband, nullptr, c->fm_stride, nullptr, 0);
     LAUNCH_CHECK();
     // squaring (:111-113) + 114 kHz BPF (:116)
-    hipLaunchKernelGGL((k_fir<1, true>), gf, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, rband, c->fm_stride,
-                       rband, c->fm_stride, c->rds_sq_h, nullptr, T, 1, n, FIR_TILE, c->plain(c->gpilot), nullptr,
-                       c->plain_stride, c->rxbuf(c->rx_rds), c->plain_stride);
+    hipLaunchKernelGGL((k_fir_rb<1, true>), gf, dim3(BLK), 0, s, rband, c->fm_stride, rband, c->fm_stride,
+                       c->rds_sq_h, nullptr, n, c->plain(c->gpilot), nullptr, c->plain_stride,
+                       c->rxbuf(c->rx_rds), c->plain_stride);
     LAUNCH_CHECK();
     c->rds_pre_done = c->block;
     return SDR_OK;
@@ -2161,18 +2410,21 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
     hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rfilt, c->rfilt + (p ^ 1) * c->rf_par,
                        c->rf_stride, in.n_rds);
     LAUNCH_CHECK();
-    const int rtile = 256;
-    dim3 gr(cdiv(in.n_rds, rtile), c->nch);
-    hipLaunchKernelGGL(k_resample<0>, gr, dim3(BLK), resample_lds_bytes(c->rdsbb_L, 247, 640, rtile, 1), s, rdc, rdc,
-                       c->fm_stride, c->fm_stride, nullptr, nullptr, (size_t)0, (size_t)0, c->rdsbb_pp,
-                       c->rdsbb_cnt, c->rdsbb_L, 247, 640, in.n_rds, rtile, -HIST, (void*)rfilt, c->rf_stride);
+    if (resample_lc_span(c->rdsbb_L, 247, 640) > 64 * RLC_XL || ((c->rdsbb_L + 3) & ~3) > 64 * RLC_HL)
+        return fail(SDR_E_INVALID, "rds_post: resampler tile does not fit (L = %d)", c->rdsbb_L);
+    dim3 gr(cdiv(in.n_rds, RLC_TN), cdiv(c->nch, 64));
+    auto kr = c->rdsbb_all101 ? k_resample_lc<101> : k_resample_lc<0>;
+    hipLaunchKernelGGL(kr, gr, dim3(BLK), resample_lc_lds_bytes(c->rdsbb_L, 247, 640), s, rdc,
+                       c->fm_stride, -HIST, c->rdsbb_pp, c->rdsbb_cnt, c->rdsbb_L, c->rds_ptq, in.n_rds, c->nch,
+                       rfilt, c->rf_stride);
     LAUNCH_CHECK();
     // RRC (:133)
-    dim3 gc(cdiv(in.n_rds, FIR_TILE), c->nch);
+    dim3 gc(cdiv(in.n_rds, FRB_TILE), c->nch);
     float* dst = rds_clean ? rds_clean : c->rds_clean;
     const size_t dst_stride = rds_clean ? rds_stride : c->clean_stride;
-    hipLaunchKernelGGL((k_fir<1, false>), gc, dim3(BLK), fir_lds_bytes(T, 1, FIR_TILE, 1), s, rfilt, c->rf_stride,
-                       rfilt, c->rf_stride, c->rrc_h, nullptr, T, 1, in.n_rds, FIR_TILE, dst, nullptr, dst_stride, nullptr, 0);
+    if (T != FRB_T) return fail(SDR_E_INVALID, "rds_post: %d taps", T);
+    hipLaunchKernelGGL((k_fir_rb<1, false>), gc, dim3(BLK), 0, s, rfilt, c->rf_stride, rfilt, c->rf_stride,
+                       c->rrc_h, nullptr, in.n_rds, dst, nullptr, dst_stride, nullptr, 0);
     LAUNCH_CHECK();
     if (rds_clean) {
         HIP_TRY(hipMemcpy2DAsync(c->rds_clean, c->clean_stride * sizeof(float), rds_clean, rds_stride * sizeof(float),
