@@ -174,7 +174,9 @@ def main() -> None:
     ev = lambda: torch.cuda.Event(enable_timing=False)  # noqa: E731
     fe_start = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
     fe_end = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
-    pre_done, pll_done, post_done, gather_done = ([ev() for _ in range(nblocks)] for _ in range(4))
+    pll_start = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
+    pre_done, post_done, gather_done = ([ev() for _ in range(nblocks)] for _ in range(3))
+    pll_done = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
     gather = None
     if world > 1 and not args.no_gather:
         from real_time_sdr_amd.sharding import BlockGather
@@ -194,6 +196,7 @@ def main() -> None:
         pipe.rds_pre(stream=s_fe)                        # rds.cpp:105-116
         pre_done[b].record(s_fe)
         s_pll.wait_event(pre_done[b])
+        pll_start[b].record(s_pll)
         pipe.plls(stream=s_pll)                          # stereo.cpp:77 + rds.cpp:119
         pll_done[b].record(s_pll)
         s_post.wait_event(pll_done[b])
@@ -234,6 +237,8 @@ def main() -> None:
     fe_avg_s = float(np.mean(fe_ms)) / 1e3
     fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
     achieved = fe_bytes / fe_avg_s / 1e9
+    # the serial PLL dispatch (both PLLs of a block) that bounds the block-step
+    pll_ms = float(np.mean([pll_start[b].elapsed_time(pll_done[b]) for b in range(args.warmup, nblocks)]))
     total_samples = world * nch * info.block_iq * args.steps
     value = total_samples / elapsed / 1e6
 
@@ -301,6 +306,15 @@ def main() -> None:
                 "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4),
             },
             "frontend_isolated": isolated or None,
+            "pll": {
+                "kernel": "k_pll: stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial "
+                          "chains in one dispatch",
+                "bound": "serial recurrence: block_if dependent steps per chain, one lane per chain "
+                         "(per-wave VALU issue and latency, DESIGN.md 4a)",
+                "avg_launch_ms": round(pll_ms, 4),
+                "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
+                "share_of_step": round(pll_ms / (elapsed / args.steps * 1e3), 4),
+            },
             "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline(),
         }
         print(json.dumps(res))

@@ -1236,9 +1236,12 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
     t_out = t;
 }
 
-constexpr int PLL_CHUNK = 16;
+#ifndef SDR_PLL_CHUNK
+#define SDR_PLL_CHUNK 16
+#endif
+constexpr int PLL_CHUNK = SDR_PLL_CHUNK;
 #ifndef SDR_PLL_NBUF
-#define SDR_PLL_NBUF 3
+#define SDR_PLL_NBUF 2
 #endif
 constexpr int PLL_NBUF = SDR_PLL_NBUF;   // register buffers of inputs (prefetch distance NBUF - 1 chunks)
 

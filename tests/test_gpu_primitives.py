@@ -105,6 +105,42 @@ def test_fmpll(pkg, oracle, torch_cuda, freq, nco, bw):
             assert st[c].phaseEst == st_ref[c].phaseEst and st[c].trigOffset == st_ref[c].trigOffset
 
 
+def test_fmpll_mixed_states(pkg, oracle, torch_cuda):
+    """Channels whose PLL states differ: distinct trigOffsets (the per-lane trigArg path instead of
+    the LDS table), states whose feedback does not match their trigArg (the fallback of the first
+    step) and a large trigOffset (coarse f32 trigArg, pll.cpp:47), bit-exact against the oracle."""
+    torch = torch_cuda
+    n = 7350
+    states = [(1.0, 0.0, 0.0, 0.0, 0.0), (1.0, 0.0, 0.0, 0.0, 12345.0),
+              (0.6, 0.8, 1e-4, 0.3, 7350.0 * 40), (1.0, 0.0, 0.0, 0.0, 3.0e6), (-1.0, 0.0, 2e-5, 2.0, 99.0)]
+    nch = len(states)
+    for freq, nco, bw in ((19e3, 2.0, 0.01), (114e3, 0.5, 0.001)):
+        arr = (pkg.PllState * nch)()
+        refs = []
+        for i, (fi, fq, ig, ph, to) in enumerate(states):
+            arr[i] = pkg.PllState(fi, fq, ig, ph, to, 1.0)
+            refs.append(oracle.PllState(fi, fq, ig, ph, to, 1.0))
+        d_st = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).cuda()
+        out_ref = [np.zeros(n + 1, np.float32) for _ in range(nch)]
+        for o in out_ref:
+            o[-1] = 1.0
+        rng = np.random.default_rng(11)
+        t = np.arange(2 * n) / 240000.0
+        for blk in range(2):
+            x = np.stack([(0.1 * np.cos(2 * np.pi * (freq + 2.0 * c) * t[blk * n:(blk + 1) * n] + 0.7 * c)
+                           + 0.01 * rng.standard_normal(n)).astype(np.float32) for c in range(nch)])
+            d_out = torch.zeros(nch, n + 1, device="cuda")
+            pkg.fmpll(d_out, torch.from_numpy(x).cuda(), freq, 240000.0, d_st, nco, 0.0, bw)
+            out = d_out.cpu().numpy()
+            for c in range(nch):
+                oracle.fmpll(x[c], freq, 240000.0, out_ref[c], refs[c], nco, 0.0, bw)
+                assert np.array_equal(_u32(out[c]), _u32(out_ref[c])), f"{freq} block {blk} ch {c}"
+            got = pkg.pll_state_from_tensor(d_st)
+            for c in range(nch):
+                for f in ("feedbackI", "feedbackQ", "integrator", "phaseEst", "trigOffset"):
+                    assert getattr(got[c], f) == getattr(refs[c], f), f"{freq} block {blk} ch {c} {f}"
+
+
 def test_cdr(pkg, oracle, torch_cuda):
     torch = torch_cuda
     rng = np.random.default_rng(9)
