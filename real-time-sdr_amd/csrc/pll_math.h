@@ -315,4 +315,157 @@ PLLM_HD Phase2 phase_detect_r(float eI0, float eQ0, double cr, double sr, double
     return phase_detect2(eI0, eQ0, cr, sr, rx, base);
 }
 
+// ------------------------------------------------------------------------------------------
+// Fallbacks: glibc's f64 results, reproduced. glibc's sin/cos/atan2 return the correctly rounded
+// f64 value RN64(f(x)) (all but a vanishing fraction of inputs), and the reference then rounds that
+// to f32. The device libm (OCML) differs from glibc by 1-2 f64 ulps on 3-27% of inputs
+// (profiles/r01/libm_flip.json); harmless on random inputs, but the fast path falls back exactly on
+// the inputs that sit next to an f32 rounding midpoint, where a 1-ulp difference flips the f32
+// result. So the fallbacks evaluate f in double-double arithmetic (error < 2^-100 relative) and
+// return its leading double, which is RN64(f(x)) -- glibc's value -- and round that to f32.
+// ------------------------------------------------------------------------------------------
+// generated by tools/pllmath/dd_consts.py
+constexpr double DD_PIO2_1 = 0x1.921fb00000000p+0;  // 22 bits
+constexpr double DD_PIO2_2 = 0x1.5110b00000000p-22;  // 22 bits
+constexpr double DD_PIO2_3 = 0x1.18469898cc517p-44;
+constexpr double DD_PIO2_4 = 0x1.b839a252049c1p-104;
+constexpr double DD_PI_HI = 0x1.921fb54442d18p+1, DD_PI_LO = 0x1.1a62633145c07p-53;
+constexpr double DD_PIO2_HI = 0x1.921fb54442d18p+0, DD_PIO2_LO = 0x1.1a62633145c07p-54;
+constexpr double DD_INV_FACT[32][2] = {
+    {0x1.0000000000000p+0, 0x0.0p+0},  // 1/0!
+    {0x1.0000000000000p+0, 0x0.0p+0},  // 1/1!
+    {0x1.0000000000000p-1, 0x0.0p+0},  // 1/2!
+    {0x1.5555555555555p-3, 0x1.5555555555555p-57},  // 1/3!
+    {0x1.5555555555555p-5, 0x1.5555555555555p-59},  // 1/4!
+    {0x1.1111111111111p-7, 0x1.1111111111111p-63},  // 1/5!
+    {0x1.6c16c16c16c17p-10, -0x1.f49f49f49f49fp-65},  // 1/6!
+    {0x1.a01a01a01a01ap-13, 0x1.a01a01a01a01ap-73},  // 1/7!
+    {0x1.a01a01a01a01ap-16, 0x1.a01a01a01a01ap-76},  // 1/8!
+    {0x1.71de3a556c734p-19, -0x1.c154f8ddc6c00p-73},  // 1/9!
+    {0x1.27e4fb7789f5cp-22, 0x1.cbbc05b4fa99ap-76},  // 1/10!
+    {0x1.ae64567f544e4p-26, -0x1.c062e06d1f209p-80},  // 1/11!
+    {0x1.1eed8eff8d898p-29, -0x1.2aec959e14c06p-83},  // 1/12!
+    {0x1.6124613a86d09p-33, 0x1.f28e0cc748ebep-87},  // 1/13!
+    {0x1.93974a8c07c9dp-37, 0x1.05d6f8a2efd1fp-92},  // 1/14!
+    {0x1.ae7f3e733b81fp-41, 0x1.1d8656b0ee8cbp-97},  // 1/15!
+    {0x1.ae7f3e733b81fp-45, 0x1.1d8656b0ee8cbp-101},  // 1/16!
+    {0x1.952c77030ad4ap-49, 0x1.ac981465ddc6cp-103},  // 1/17!
+    {0x1.6827863b97d97p-53, 0x1.eec01221a8b0bp-107},  // 1/18!
+    {0x1.2f49b46814157p-57, 0x1.2650f61dbdcb4p-112},  // 1/19!
+    {0x1.e542ba4020225p-62, 0x1.ea72b4afe3c2fp-120},  // 1/20!
+    {0x1.71b8ef6dcf572p-66, -0x1.d043ae40c4647p-120},  // 1/21!
+    {0x1.0ce396db7f853p-70, -0x1.aebcdbd20331cp-124},  // 1/22!
+    {0x1.761b41316381ap-75, -0x1.3423c7d91404fp-130},  // 1/23!
+    {0x1.f2cf01972f578p-80, -0x1.9ada5fcc1ab14p-135},  // 1/24!
+    {0x1.3f3ccdd165fa9p-84, -0x1.58ddadf344487p-139},  // 1/25!
+    {0x1.88e85fc6a4e5ap-89, -0x1.71c37ebd16540p-143},  // 1/26!
+    {0x1.d1ab1c2dccea3p-94, 0x1.054d0c78aea14p-149},  // 1/27!
+    {0x1.0a18a2635085dp-98, 0x1.b9e2e28e1aa54p-153},  // 1/28!
+    {0x1.259f98b4358adp-103, 0x1.eaf8c39dd9bc5p-157},  // 1/29!
+    {0x1.3932c5047d60ep-108, 0x1.832b7b530a627p-162},  // 1/30!
+    {0x1.434d2e783f5bcp-113, 0x1.0b87b91be9affp-167},  // 1/31!
+};
+
+struct DD {
+    double hi, lo;
+};
+PLLM_HD DD two_sum(double a, double b) {
+    const double s = a + b;
+    const double bb = s - a;
+    return {s, (a - (s - bb)) + (b - bb)};
+}
+PLLM_HD DD quick_two_sum(double a, double b) {  // |a| >= |b|
+    const double s = a + b;
+    return {s, b - (s - a)};
+}
+PLLM_HD DD two_prod(double a, double b) {
+    const double p = a * b;
+    return {p, fma_(a, b, -p)};
+}
+PLLM_HD DD dd_add(DD a, DD b) {
+    DD s = two_sum(a.hi, b.hi);
+    const DD t = two_sum(a.lo, b.lo);
+    s.lo += t.hi;
+    s = quick_two_sum(s.hi, s.lo);
+    s.lo += t.lo;
+    return quick_two_sum(s.hi, s.lo);
+}
+PLLM_HD DD dd_neg(DD a) { return {-a.hi, -a.lo}; }
+PLLM_HD DD dd_mul(DD a, DD b) {
+    DD p = two_prod(a.hi, b.hi);
+    p.lo += a.hi * b.lo + a.lo * b.hi;
+    return quick_two_sum(p.hi, p.lo);
+}
+PLLM_HD DD dd_mul_d(DD a, double b) {
+    DD p = two_prod(a.hi, b);
+    p.lo += a.lo * b;
+    return quick_two_sum(p.hi, p.lo);
+}
+PLLM_HD DD dd_div(DD a, DD b) {
+    const double q1 = a.hi / b.hi;
+    DD r = dd_add(a, dd_neg(dd_mul_d(b, q1)));
+    const double q2 = r.hi / b.hi;
+    r = dd_add(r, dd_neg(dd_mul_d(b, q2)));
+    const double q3 = r.hi / b.hi;
+    return dd_add(quick_two_sum(q1, q2), DD{q3, 0.0});
+}
+
+// sum_{k<=14} (-1)^k z^k / (2k+o)!  (o = 0: cos r, o = 1: sin r / r), Horner; |z| <= 0.62 leaves
+// a truncation error below 2^-110
+PLLM_HD DD dd_trig_series(DD z, int o) {
+    DD p = {DD_INV_FACT[28 + o][0], DD_INV_FACT[28 + o][1]};
+    for (int k = 13; k >= 0; k--) {
+        p = dd_mul(p, dd_neg(z));
+        p = dd_add(p, DD{DD_INV_FACT[2 * k + o][0], DD_INV_FACT[2 * k + o][1]});
+    }
+    return p;
+}
+
+// cos t, sin t in double-double for |t| < 2^30, t a double for which t - k*P1 below is exact
+// (f32 arguments, or any |t| <= 4). Reduction by the 22/22/53/53-bit pi/2 split: k*P1 and k*P2
+// are exact; the rest in double-double (error < 2^-125 absolute).
+PLLM_HD void dd_sincos_dd(double t, DD& c, DD& s) {
+    const double kd = __builtin_rint(t * TWO_OVER_PI);
+    const double a = fma_(-kd, DD_PIO2_1, t);
+    DD r = two_sum(a, -(kd * DD_PIO2_2));
+    r = dd_add(r, dd_neg(two_prod(kd, DD_PIO2_3)));
+    r = dd_add(r, DD{-(kd * DD_PIO2_4), 0.0});
+    const DD z = dd_mul(r, r);
+    const DD cr = dd_trig_series(z, 0);
+    const DD sr = dd_mul(dd_trig_series(z, 1), r);
+    // cos t + i sin t = i^q (cos r + i sin r)
+    switch ((int)kd & 3) {
+        case 0: c = cr; s = sr; break;
+        case 1: c = dd_neg(sr); s = cr; break;
+        case 2: c = dd_neg(cr); s = dd_neg(sr); break;
+        default: c = sr; s = dd_neg(cr); break;
+    }
+}
+
+// RN64(cos t), RN64(sin t): glibc's cos/sin of pll.cpp:49-50 and :52
+PLLM_HD void dd_sincos(double t, double* s_out, double* c_out) {
+    DD c, s;
+    dd_sincos_dd(t, c, s);
+    *c_out = c.hi;
+    *s_out = s.hi;
+}
+
+// RN64(atan2(y, x)) (glibc's atan2 of pll.cpp:39) for f32 inputs. th0 is any approximation within a
+// few ulps (the device libm's); rotating (x, y) by -th0 in double-double leaves a residual angle
+// |d| < 2^-48, and atan2(y, x) = th0 + d - d^3/3 to 2^-140. Zeros, infinities and NaN return th0:
+// their results are exact special values in every libm.
+PLLM_HD double dd_atan2_f32(float y, float x, double th0) {
+    if (!(__builtin_fabs(th0) <= 4.0) || (x == 0.0f && y == 0.0f) || !(__builtin_fabs(x) < 0x1p127f) ||
+        !(__builtin_fabs(y) < 0x1p127f))
+        return th0;
+    DD c, s;
+    dd_sincos_dd(th0, c, s);
+    // (X + iY) = (x + iy)(c - is)
+    const DD X = dd_add(dd_mul_d(c, (double)x), dd_mul_d(s, (double)y));
+    const DD Y = dd_add(dd_mul_d(c, (double)y), dd_neg(dd_mul_d(s, (double)x)));
+    const DD d = dd_div(Y, X);
+    const double d3 = d.hi * d.hi * d.hi * (1.0 / 3.0);
+    return dd_add(two_sum(th0, d.hi), DD{d.lo - d3, 0.0}).hi;
+}
+
 }  // namespace pllm

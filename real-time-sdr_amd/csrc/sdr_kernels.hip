@@ -1176,10 +1176,20 @@ __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& 
            (TAB || (__builtin_fabs(w) * (__builtin_fabs(r.toff) + (double)chunk) < 0x1p29));
 }
 
-// the f64 libm of the reference step (pll.cpp:39, :49-50), out of line: only the rare fallbacks
-// call them, and the unrolled redo chunks stay small
-__device__ __noinline__ float pll_atan2_ref(float eQ, float eI) { return (float)atan2((double)eQ, (double)eI); }
-__device__ __noinline__ void pll_sincos_ref(float t, double* s, double* c) { sincos((double)t, s, c); }
+// the f64 libm results of the reference step (pll.cpp:39, :49-50), out of line: only the rare
+// fallbacks call them, and the unrolled redo chunks stay small. They return glibc's value RN64(f)
+// from double-double evaluations (pll_math.h), not the device libm's, which differs from glibc by
+// 1-2 ulps on 3-27% of inputs -- enough to flip an f32 rounding on the near-midpoint inputs that
+// reach a fallback. |t| >= 2^30 (beyond the reduction) keeps the device libm.
+__device__ __noinline__ float pll_atan2_ref(float eQ, float eI) {
+    return (float)pllm::dd_atan2_f32(eQ, eI, atan2((double)eQ, (double)eI));
+}
+__device__ __noinline__ void pll_sincos_ref(float t, double* s, double* c) {
+    if (__builtin_fabs(t) < 0x1p30f)
+        pllm::dd_sincos((double)t, s, c);
+    else
+        sincos((double)t, s, c);
+}
 
 // One step of pll.cpp:36-50. CHECKED: every result the fast path cannot prove is recomputed
 // with the f64 libm exactly as the reference (used for chunk redo and short tails).
@@ -1438,6 +1448,13 @@ __global__ __launch_bounds__(64) void k_pll_libm(const PllJobs jobs, int n, int 
     st[ch].trigOffset = toff;
 }
 
+// glibc's cos of pll.cpp:52 for the inputs the fast path cannot decide (see pll_atan2_ref)
+__device__ __noinline__ float nco_cos_ref(float a) {
+    double sv, cv;
+    pll_sincos_ref(a, &sv, &cv);
+    return (float)cv;
+}
+
 // out[ch][i+1]: t_i -> (float)cos((double)(t_i*ncoScale + phaseAdjust)) (pll.cpp:52), in parallel;
 // lastCarrier <- out[ch][n] (pll.cpp:58)
 __global__ __launch_bounds__(BLK) void k_nco_out(const PllJobs jobs, int n) {
@@ -1455,7 +1472,7 @@ __global__ __launch_bounds__(BLK) void k_nco_out(const PllJobs jobs, int n) {
     const float a = t * ncoScale + phaseAdjust;
     const pllm::SinCos sc = pllm::sincos_f32(a);
     float v = (float)sc.c;
-    if (!sc.ok) v = (float)cos((double)a);
+    if (!sc.ok) v = nco_cos_ref(a);
     o[i] = v;
     if (i == n - 1) st[ch].lastCarrier = v;
     if (i == 0 && jb.prev_out) o[-1] = jb.prev_out[(size_t)ch * out_stride + n];

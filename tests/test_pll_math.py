@@ -1,0 +1,33 @@
+"""Host checks of the PLL math shared with the kernels (real-time-sdr_amd/csrc/pll_math.h).
+
+The double-double fallbacks must reproduce glibc's f64 sin/cos/atan2 (the reference's libm,
+pll.cpp:39, :49-52) after the f32 rounding the reference applies: tools/pllmath/validate_dd.cpp
+compares them with this host's glibc on random PLL-like arguments and on arguments whose cosine
+lies next to an f32 rounding midpoint, and fails on any f32 difference. The same header is
+compiled for the device; the device results are compared with glibc by tools/pllmath/libm_flip.hip
+(profiles/r01/libm_flip.json).
+"""
+from __future__ import annotations
+
+import json
+import pathlib
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_dd_fallbacks_match_glibc(tmp_path):
+    exe = tmp_path / "validate_dd"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", str(ROOT / "real-time-sdr_amd/csrc"),
+                    str(ROOT / "tools/pllmath/validate_dd.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "300000"], capture_output=True, text=True, timeout=120)
+    res = json.loads(r.stdout)
+    assert r.returncode == 0, res
+    for f in ("cos", "sin", "atan2"):
+        assert res[f]["f32_mismatch"] == 0
+        # f64 differences are glibc's own misroundings (|err| just over 0.5 ulp): rare
+        assert res[f]["f64_mismatch"] < 0.005 * res["n"]
