@@ -46,16 +46,44 @@ def _load_pkg():
     return mod
 
 
-def make_input(torch, nch: int, nblocks: int, first_channel: int, device):
-    """[nblocks][nch][2*73500] u8 on the device. A few hundred distinct channels are synthesised and
-    tiled across the batch (each channel stays a continuous FM stream across blocks)."""
-    import real_time_sdr_amd.synth as synth
+def _synth_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("sdr_synth", ROOT / "real-time-sdr_amd" / "synth.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _synth_channel(channel: int, nblocks: int) -> np.ndarray:
+    """nblocks consecutive u8 I/Q blocks of one synthetic channel (numpy only, no GPU)."""
+    synth = _synth_module()
+    src = synth.FMMultiplexSource(channel)
+    return np.stack([src.next_block() for _ in range(nblocks)])
+
+
+def synth_host_input(nch: int, nblocks: int, first_channel: int) -> np.ndarray:
+    """[nblocks][distinct][2*73500] u8 on the host for min(nch, 16) distinct channels, synthesised in
+    child processes (about 23 ms per channel-block; call before the GPU is initialised)."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
     distinct = min(nch, 16)
-    host = np.empty((nblocks, distinct, 2 * synth.BLOCK_IQ), np.uint8)
-    for c in range(distinct):
-        src = synth.FMMultiplexSource(first_channel + c)
-        for b in range(nblocks):
-            host[b, c] = src.next_block()
+    workers = max(1, min(distinct, 8, os.cpu_count() or 1))
+    if workers == 1 or nblocks * distinct < 64:
+        chans = [_synth_channel(first_channel + c, nblocks) for c in range(distinct)]
+    else:
+        with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn")) as ex:
+            chans = list(ex.map(_synth_channel, [first_channel + c for c in range(distinct)],
+                                [nblocks] * distinct))
+    return np.ascontiguousarray(np.stack(chans, axis=1))
+
+
+def make_input(torch, nch: int, nblocks: int, first_channel: int, device, host: np.ndarray | None = None):
+    """[nblocks][nch][2*73500] u8 on the device. A few distinct channels are synthesised and tiled
+    across the batch (each channel stays a continuous FM stream across blocks)."""
+    synth = _synth_module()
+    if host is None:
+        host = synth_host_input(nch, nblocks, first_channel)
+    distinct = host.shape[1]
     # rows padded to a multiple of 16 bytes (147008 for 147000): the front end then stages whole
     # 16-byte I/Q groups
     row = 2 * synth.BLOCK_IQ
@@ -130,8 +158,8 @@ def _cpu_model() -> str:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--channels", type=int, default=1024, help="channels per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL gather (N>1)")
@@ -141,12 +169,16 @@ def main() -> None:
                          "(fm_demod within 1e-5, RDS bits bit-exact)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    nblocks = args.warmup + args.steps
+    # this rank's synthetic input, made in child processes before anything touches the GPU
+    host_iq = synth_host_input(args.channels, nblocks, first_channel=rank * args.channels)
+
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -154,11 +186,11 @@ def main() -> None:
     torch.cuda.set_device(dev)
     pkg = _load_pkg()
 
-    nch = args.channels
-    nblocks = args.warmup + args.steps
     from real_time_sdr_amd.sharding import channel_range
-    first, nch = channel_range(nch, rank)
-    iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
+    first, nch = channel_range(args.channels, rank)
+    assert first == rank * args.channels
+    iq = make_input(torch, nch, nblocks, first_channel=first, device=dev, host=host_iq)
+    del host_iq
     fast = args.numerics == "fast"
     pipe = pkg.Pipeline(nch, mode=0, rds_on=True, device=local, flags=pkg.FLAG_FAST_FRONTEND if fast else 0)
     info = pipe.info
@@ -166,7 +198,9 @@ def main() -> None:
     # stream; a fourth stream would share a queue and serialise behind it): front end + mono + the
     # FIRs feeding both PLLs; both PLLs in one dispatch; everything after the PLLs. The serial PLLs
     # bound the step, so they run back to back across blocks while the other streams fill the chip.
-    s_fe, s_pll, s_post = (torch.cuda.Stream(dev) for _ in range(3))
+    # SDR_BENCH_PRIO (A/B): comma list of streams (fe, pll, post) created with high priority
+    prio = set(filter(None, os.environ.get("SDR_BENCH_PRIO", "").split(",")))
+    s_fe, s_pll, s_post = (torch.cuda.Stream(dev, priority=-1 if n in prio else 0) for n in ("fe", "pll", "post"))
     mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
     lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]
     bits = [torch.empty(nch, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -174,9 +208,11 @@ def main() -> None:
     ev = lambda: torch.cuda.Event(enable_timing=False)  # noqa: E731
     fe_start = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
     fe_end = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
-    pll_start = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
+    # SDR_BENCH_PLL_TIMING=0 (A/B): no timestamp packets on the PLL stream (pll object omitted)
+    pll_timing = os.environ.get("SDR_BENCH_PLL_TIMING", "1") != "0"
+    pll_start = [torch.cuda.Event(enable_timing=pll_timing) for _ in range(nblocks)]
     pre_done, post_done, gather_done = ([ev() for _ in range(nblocks)] for _ in range(3))
-    pll_done = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
+    pll_done = [torch.cuda.Event(enable_timing=pll_timing) for _ in range(nblocks)]
     gather = None
     if world > 1 and not args.no_gather:
         from real_time_sdr_amd.sharding import BlockGather
@@ -238,7 +274,8 @@ def main() -> None:
     fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
     achieved = fe_bytes / fe_avg_s / 1e9
     # the serial PLL dispatch (both PLLs of a block) that bounds the block-step
-    pll_ms = float(np.mean([pll_start[b].elapsed_time(pll_done[b]) for b in range(args.warmup, nblocks)]))
+    pll_ms = (float(np.mean([pll_start[b].elapsed_time(pll_done[b]) for b in range(args.warmup, nblocks)]))
+              if pll_timing else float("nan"))
     total_samples = world * nch * info.block_iq * args.steps
     value = total_samples / elapsed / 1e6
 
