@@ -271,17 +271,24 @@ struct SinCosR {
     double cr, sr;   // cos r, sin r (relative error < 2^-50)
     double mr;       // -r
     uint32_t q, b;   // quadrant, [r < 0]
-    uint32_t tie;    // min(tie_distance64(cr), tie_distance64(sr))
+    uint32_t tie;    // min(tie_key64(cr), tie_key64(sr)); the roundings are safe iff tie > TIE_MIN
 };
+
+// 8 x tie_distance64(v) (mod 2^32) in one shift-add: the shift drops the 3 low f32 mantissa bits
+// that sit above the 29-bit field. tie_distance64(v) > 128 <=> tie_key64(v) > TIE_MIN.
+constexpr uint32_t TIE_MIN = 128u << 3;
+PLLM_HD uint32_t tie_key64(double v) { return ((uint32_t)__builtin_bit_cast(uint64_t, v) << 3) + 0x80000200u; }
+
+// pi/2 as RN64 + the f64 rest: with t an f32 and |t| < 2^30, t - kd*PIO2_HI is exact (a multiple of
+// 2^-52 below 1 in magnitude), so two fmas reduce with one rounding plus |kd| 2^-107
+constexpr double PIO2_HI = 0x1.921fb54442d18p+0, PIO2_LO = 0x1.1a62633145c07p-54;
 
 // valid for |t| < T_MAX (the caller checks the range)
 PLLM_HD SinCosR sincos_r(float t) {
     const double x = (double)t;
     const double kdp = fma_(x, TWO_OVER_PI, MAGIC);
     const double kd = kdp - MAGIC;
-    double r = fma_(-kd, P1, x);
-    r = fma_(-kd, P2, r);
-    r = fma_(-kd, P3, r);
+    const double r = fma_(-kd, PIO2_LO, fma_(-kd, PIO2_HI, x));
     const double z = r * r;
     const double z2 = z * z;
     const double z4 = z2 * z2;
@@ -293,7 +300,7 @@ PLLM_HD SinCosR sincos_r(float t) {
     o.mr = -r;
     o.q = (uint32_t)__builtin_bit_cast(uint64_t, kdp);
     o.b = (uint32_t)(__builtin_bit_cast(uint64_t, r) >> 63);
-    const uint32_t tc = tie_distance64(o.cr), ts = tie_distance64(o.sr);
+    const uint32_t tc = tie_key64(o.cr), ts = tie_key64(o.sr);
     o.tie = tc < ts ? tc : ts;
     return o;
 }

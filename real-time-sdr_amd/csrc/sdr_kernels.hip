@@ -1133,7 +1133,7 @@ __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
     const pllm::SinCosR sc = pllm::sincos_r(t_prev);
     float fI = (float)sc.cr, fQ = (float)sc.sr;
     pllm::rot_q(sc.q, fI, fQ);
-    const bool consistent = (__builtin_fabs((double)t_prev) < pllm::T_MAX) && sc.tie > 128u &&
+    const bool consistent = (__builtin_fabs((double)t_prev) < pllm::T_MAX) && sc.tie > pllm::TIE_MIN &&
                             fI == st.feedbackI && fQ == st.feedbackQ;
     if (consistent) {
         r.fbI = (float)sc.cr;
@@ -1171,7 +1171,7 @@ struct PllProof {
 // TAB: the trigArg offsets come from a table whose range the kernel checked once (pll_run)
 template <bool TAB>
 __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
-    return (pf.emax < pllm::PI - 0x1p-30) & (pf.split == 0u) & (pf.tie > 128u) &
+    return (pf.emax < pllm::PI - 0x1p-30) & (pf.split == 0u) & (pf.tie > pllm::TIE_MIN) &
            (__builtin_fabs(r.ph) < 0x1p28f) & (__builtin_fabs(r.integ) < 0x1p20f) &
            (TAB || (__builtin_fabs(w) * (__builtin_fabs(r.toff) + (double)chunk) < 0x1p29));
 }
@@ -1228,7 +1228,7 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
     r.fbQ = (float)sc.sr;
     if (CHECKED) {
         const bool in_range = __builtin_fabs((double)t) < pllm::T_MAX;
-        if (!(in_range && sc.tie > 128u)) {
+        if (!(in_range && sc.tie > pllm::TIE_MIN)) {
             double sv, cv;
             pll_sincos_ref(t, &sv, &cv);
             pllm::rot_q(0u - r.q, cv, sv);                    // into the reduced frame, exactly

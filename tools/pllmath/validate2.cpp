@@ -41,6 +41,34 @@ int main(int argc, char** argv) {
     }
     std::printf("sincos2: ok %ld fallback %ld (%.2e) mismatches %ld\n", sc_ok, sc_bad, (double)sc_bad / N, sc_mis);
 
+    // 1b) the reduced-frame sincos_r (k_pll) on the same argument mix: accepted roundings, rotated
+    // by i^q, must equal RN_f32(glibc cos t), RN_f32(glibc sin t)
+    {
+        long ok = 0, bad = 0, mis = 0;
+        std::mt19937_64 rng2(4242);
+        for (long i = 0; i < N; i++) {
+            float t;
+            if (i % 4 == 3) {
+                const double k = std::floor(U(rng2) * 6.8e8);
+                t = std::nextafter((float)(k * pllm::PIO2), (float)((i & 8) ? 1e10 : -1e10));
+            } else {
+                t = (float)(std::exp2(-30.0 + 60.0 * U(rng2)) * ((i & 1) ? 1 : -1));
+            }
+            if (!(std::fabs(t) < pllm::T_MAX)) continue;
+            const pllm::SinCosR r = pllm::sincos_r(t);
+            if (!(r.tie > pllm::TIE_MIN)) { bad++; continue; }
+            ok++;
+            float c = (float)r.cr, sn = (float)r.sr;
+            pllm::rot_q(r.q, c, sn);
+            if (c != (float)std::cos((double)t) || sn != (float)std::sin((double)t)) {
+                if (mis < 10) std::printf("sincos_r MISMATCH t=%.9g\n", t);
+                mis++;
+            }
+        }
+        std::printf("sincos_r: ok %ld fallback %ld (%.2e) mismatches %ld\n", ok, bad, (double)bad / N, mis);
+        sc_mis += mis;
+    }
+
     // 2) phase detector v2 on (eI, eQ) = x (RN cos t, -RN sin t), base from the same t
     long pd_ok = 0, pd_bad = 0, pd_mis = 0;
     double dmax = 0.0;
@@ -119,7 +147,7 @@ int main(int argc, char** argv) {
                 sc = pllm::sincos2_f32(t);
                 c = sc.c; s = sc.s;
                 fbI = (float)c; fbQ = (float)s;
-                if (!(sc.tie > 128u)) {
+                if (!(sc.tie > pllm::TIE_MIN)) {
                     c = std::cos((double)t); s = std::sin((double)t);
                     fbI = (float)c; fbQ = (float)s;
                     fb_sc++;
@@ -191,7 +219,7 @@ int main(int argc, char** argv) {
                 sc = pllm::sincos_r(t);
                 cr = sc.cr; sr = sc.sr; mr = sc.mr; q = sc.q; bsg = sc.b;
                 fI0 = (float)cr; fQ0 = (float)sr;
-                if (!(sc.tie > 128u)) {
+                if (!(sc.tie > pllm::TIE_MIN)) {
                     double cv = std::cos((double)t), sv = std::sin((double)t);
                     pllm::rot_q(0u - q, cv, sv);
                     cr = cv; sr = sv;
