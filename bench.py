@@ -46,6 +46,55 @@ def _load_pkg():
     return mod
 
 
+def cu_masked_streams(torch, pkg, dev, spec: str):
+    """(fe, pll, post) streams with disjoint CU masks (hipExtStreamCreateWithCUMask, resolved
+    through libsdr_amd.so's handle so that it is the HIP runtime torch and the kernels use)."""
+    import ctypes as C
+    n, _, stride = spec.partition(":")
+    n, stride = int(n), int(stride or 1)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    pll_bits = [i * stride for i in range(n)]
+    if n <= 0 or pll_bits[-1] >= ncu:
+        raise ValueError(f"SDR_BENCH_CUMASK={spec}: needs n*stride <= {ncu} CUs")
+    words = (ncu + 31) // 32
+    pll_mask = [0] * words
+    for bit in pll_bits:
+        pll_mask[bit // 32] |= 1 << (bit % 32)
+    full = [0xFFFFFFFF] * words
+    if ncu % 32:
+        full[-1] = (1 << (ncu % 32)) - 1
+    rest_mask = [f & ~p for f, p in zip(full, pll_mask)]
+    create = pkg.lib().hipExtStreamCreateWithCUMask
+    create.restype = C.c_int
+    create.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_uint32)]
+    out = []
+    for mask in (rest_mask, pll_mask, rest_mask):
+        h = C.c_void_p()
+        arr = (C.c_uint32 * words)(*mask)
+        rc = create(C.byref(h), words, arr)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+        _MASKED_STREAMS.append(h.value)
+        out.append(torch.cuda.ExternalStream(h.value, device=dev))
+    return tuple(out)
+
+
+_MASKED_STREAMS: list[int] = []
+
+
+def destroy_masked_streams(torch, pkg, dev) -> None:
+    """hipStreamDestroy the streams cu_masked_streams made (torch does not own them)."""
+    import ctypes as C
+    if not _MASKED_STREAMS:
+        return
+    torch.cuda.synchronize(dev)
+    destroy = pkg.lib().hipStreamDestroy
+    destroy.restype = C.c_int
+    destroy.argtypes = [C.c_void_p]
+    while _MASKED_STREAMS:
+        destroy(C.c_void_p(_MASKED_STREAMS.pop()))
+
+
 def _synth_module():
     import importlib.util
     spec = importlib.util.spec_from_file_location("sdr_synth", ROOT / "real-time-sdr_amd" / "synth.py")
@@ -201,6 +250,14 @@ def main() -> None:
     # SDR_BENCH_PRIO (A/B): comma list of streams (fe, pll, post) created with high priority
     prio = set(filter(None, os.environ.get("SDR_BENCH_PRIO", "").split(",")))
     s_fe, s_pll, s_post = (torch.cuda.Stream(dev, priority=-1 if n in prio else 0) for n in ("fe", "pll", "post"))
+    # SDR_BENCH_CUMASK=<n>[:stride] (default 64; 0 = no masks): the PLL stream gets n CUs of its
+    # own (CU-mask bits 0, stride, 2*stride, ...), the front-end and post streams the complement,
+    # so that no other kernel shares a CU's issue slots with the PLL's 32 lone waves. Measured
+    # (profiles/r01/ab_cumask.txt): none 0.895 ms/step, 8 CUs 1.86, 16 0.99, 32 0.871, 48-96
+    # 0.864-0.870, 128 0.911 (front end starved)
+    cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64")
+    if cu_spec not in ("", "0"):
+        s_fe, s_pll, s_post = cu_masked_streams(torch, pkg, dev, cu_spec)
     mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
     lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]
     bits = [torch.empty(nch, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -331,6 +388,8 @@ def main() -> None:
                             f"{nch} channels/GPU, mode 0 (2.4 MS/s, 73500 I/Q per block)",
                 "channels_per_gpu": nch, "channels_total": world * nch, "block_iq": info.block_iq,
                 "mode": 0,
+                "pll_cus": (f"PLL stream on CU-mask {cu_spec}, other streams on the rest"
+                            if cu_spec not in ("", "0") else "no CU masks"),
                 "numerics": ("fast: int8 MFMA front end, fm_demod within 1e-5 of the reference, RDS bits bit-exact"
                              if fast else "exact (bit-exact with the reference)"),
                 "parallelism": f"channel-sharded x{world}" + ("" if world == 1 or args.no_gather else " + RCCL all-gather"),
@@ -356,6 +415,7 @@ def main() -> None:
         }
         print(json.dumps(res))
     pipe.close()
+    destroy_masked_streams(torch, pkg, dev)
     if world > 1:
         dist.destroy_process_group()
 
