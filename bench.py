@@ -257,7 +257,12 @@ def main() -> None:
     # 0.864-0.870, 128 0.911 (front end starved)
     cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64")
     if cu_spec not in ("", "0"):
-        s_fe, s_pll, s_post = cu_masked_streams(torch, pkg, dev, cu_spec)
+        try:
+            s_fe, s_pll, s_post = cu_masked_streams(torch, pkg, dev, cu_spec)
+        except (RuntimeError, ValueError, AttributeError) as exc:   # plain streams, reported
+            print(f"bench: CU-masked streams unavailable ({exc}); unmasked streams", file=sys.stderr)
+            destroy_masked_streams(torch, pkg, dev)
+            cu_spec = ""
     mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
     lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]
     bits = [torch.empty(nch, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev) for _ in range(2)]
