@@ -47,33 +47,19 @@ def _load_pkg():
 
 
 def cu_masked_streams(torch, pkg, dev, spec: str):
-    """(fe, pll, post) streams with disjoint CU masks (hipExtStreamCreateWithCUMask, resolved
-    through libsdr_amd.so's handle so that it is the HIP runtime torch and the kernels use)."""
+    """(fe, pll, post) streams on disjoint CUs through the C ABI (sdr_stream_create_cu_range):
+    the PLL stream on CUs [0, n), the other two on the rest."""
     import ctypes as C
-    n, _, stride = spec.partition(":")
-    n, stride = int(n), int(stride or 1)
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    pll_bits = [i * stride for i in range(n)]
-    if n <= 0 or pll_bits[-1] >= ncu:
-        raise ValueError(f"SDR_BENCH_CUMASK={spec}: needs n*stride <= {ncu} CUs")
-    words = (ncu + 31) // 32
-    pll_mask = [0] * words
-    for bit in pll_bits:
-        pll_mask[bit // 32] |= 1 << (bit % 32)
-    full = [0xFFFFFFFF] * words
-    if ncu % 32:
-        full[-1] = (1 << (ncu % 32)) - 1
-    rest_mask = [f & ~p for f, p in zip(full, pll_mask)]
-    create = pkg.lib().hipExtStreamCreateWithCUMask
-    create.restype = C.c_int
-    create.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_uint32)]
+    n = int(spec)
+    L = pkg.lib()
+    L.sdr_stream_create_cu_range.restype = C.c_int
+    L.sdr_stream_create_cu_range.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int]
     out = []
-    for mask in (rest_mask, pll_mask, rest_mask):
+    for exclude in (1, 0, 1):
         h = C.c_void_p()
-        arr = (C.c_uint32 * words)(*mask)
-        rc = create(C.byref(h), words, arr)
+        rc = L.sdr_stream_create_cu_range(C.byref(h), dev.index, 0, n, exclude)
         if rc != 0:
-            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+            raise RuntimeError(f"sdr_stream_create_cu_range: {rc} {L.sdr_last_error()}")
         _MASKED_STREAMS.append(h.value)
         out.append(torch.cuda.ExternalStream(h.value, device=dev))
     return tuple(out)
@@ -83,16 +69,16 @@ _MASKED_STREAMS: list[int] = []
 
 
 def destroy_masked_streams(torch, pkg, dev) -> None:
-    """hipStreamDestroy the streams cu_masked_streams made (torch does not own them)."""
+    """sdr_stream_destroy the streams cu_masked_streams made (torch does not own them)."""
     import ctypes as C
     if not _MASKED_STREAMS:
         return
     torch.cuda.synchronize(dev)
-    destroy = pkg.lib().hipStreamDestroy
-    destroy.restype = C.c_int
-    destroy.argtypes = [C.c_void_p]
+    L = pkg.lib()
+    L.sdr_stream_destroy.restype = C.c_int
+    L.sdr_stream_destroy.argtypes = [C.c_void_p]
     while _MASKED_STREAMS:
-        destroy(C.c_void_p(_MASKED_STREAMS.pop()))
+        L.sdr_stream_destroy(C.c_void_p(_MASKED_STREAMS.pop()))
 
 
 def _synth_module():
@@ -250,8 +236,8 @@ def main() -> None:
     # SDR_BENCH_PRIO (A/B): comma list of streams (fe, pll, post) created with high priority
     prio = set(filter(None, os.environ.get("SDR_BENCH_PRIO", "").split(",")))
     s_fe, s_pll, s_post = (torch.cuda.Stream(dev, priority=-1 if n in prio else 0) for n in ("fe", "pll", "post"))
-    # SDR_BENCH_CUMASK=<n>[:stride] (default 64; 0 = no masks): the PLL stream gets n CUs of its
-    # own (CU-mask bits 0, stride, 2*stride, ...), the front-end and post streams the complement,
+    # SDR_BENCH_CUMASK=<n> (default 64; 0 = no masks): the PLL stream gets CUs [0, n) of its
+    # own, the front-end and post streams the complement,
     # so that no other kernel shares a CU's issue slots with the PLL's 32 lone waves. Measured
     # (profiles/r01/ab_cumask.txt): none 0.895 ms/step, 8 CUs 1.86, 16 0.99, 32 0.871, 48-96
     # 0.864-0.870, 128 0.911 (front end starved)

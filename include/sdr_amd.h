@@ -160,6 +160,15 @@ int sdr_get_fm_demod(sdr_ctx *ctx, float *fm, size_t fm_stride, void *stream);
  * "gen_pilot","ipll","rds_dc","rds_filt","rds_clean","stereo_dc"}; *stride in elements. */
 int sdr_ctx_buffer(sdr_ctx *ctx, const char *name, const float **ptr, size_t *stride, int *len);
 
+/* Streams on disjoint CU sets (no reference counterpart: the reference's three threads,
+ * project.cpp:134-136, share one CPU; this is their placement on the GPU). Creates a HIP stream
+ * on `device` whose kernels run only on CU-mask bits [first_cu, first_cu + n_cu) (exclude = 0),
+ * or on every CU except those (exclude = 1). Giving the serial PLL stream (sdr_plls) its own CUs
+ * keeps the other stages' kernels off the SIMDs its lone waves issue from.
+ * Release with sdr_stream_destroy. */
+int sdr_stream_create_cu_range(void **stream, int device, int first_cu, int n_cu, int exclude);
+int sdr_stream_destroy(void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1997,6 +1997,32 @@ extern "C" {
 const char* sdr_last_error(void) { return g_err.c_str(); }
 int sdr_version(void) { return 1; }
 
+int sdr_stream_create_cu_range(void** stream, int device, int first_cu, int n_cu, int exclude) {
+    if (!stream) return fail(SDR_E_INVALID, "sdr_stream_create_cu_range: stream is NULL");
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    const int ncu = prop.multiProcessorCount;
+    if (first_cu < 0 || n_cu <= 0 || first_cu + n_cu > ncu || (exclude && n_cu >= ncu))
+        return fail(SDR_E_INVALID, "sdr_stream_create_cu_range: CUs [%d, %d) outside [0, %d)",
+                    first_cu, first_cu + n_cu, ncu);
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int cu = 0; cu < ncu; ++cu) {
+        const bool in = cu >= first_cu && cu < first_cu + n_cu;
+        if (in != (exclude != 0)) mask[cu / 32] |= 1u << (cu % 32);
+    }
+    hipStream_t s = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    *stream = s;
+    return SDR_OK;
+}
+
+int sdr_stream_destroy(void* stream) {
+    if (!stream) return fail(SDR_E_INVALID, "sdr_stream_destroy: stream is NULL");
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return SDR_OK;
+}
+
 int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int flags) {
     if (!out || nch <= 0) return fail(SDR_E_INVALID, "bad arguments");
     *out = nullptr;

@@ -32,6 +32,9 @@ def test_errors_are_status_codes(pkg):
     assert lib.sdr_frontend(None, None, 0, None) == -1
     assert lib.sdr_convolve_fir(None, 0, None, 0, 1, 10, None, 101, None, 100, 1, None) == -1
     assert lib.sdr_impulse_response_lpf(2.4e6, 1e5, 101, None) == -1
+    assert lib.sdr_stream_create_cu_range(None, 0, 0, 64, 0) == -1   # NULL out: no HIP call made
+    assert lib.sdr_stream_destroy(None) == -1
+    assert b"NULL" in lib.sdr_last_error()
 
 
 def test_product_taps_equal_reference_taps(pkg, golden):

@@ -214,8 +214,9 @@ def test_fast_frontend_tolerance_and_rds_bits(pkg, synth, golden_long, oracle, t
                 assert _bitstr(out["bits"][b][j], int(out["nbits"][b][j])) == want["bits"], f"bits ch{c} block {b}"
 
 
-@pytest.mark.parametrize("fused_plls", [False, True], ids=["two_pll_streams", "sdr_plls"])
-def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_plls):
+@pytest.mark.parametrize("fused_plls,cu_masked", [(False, False), (True, False), (True, True)],
+                         ids=["two_pll_streams", "sdr_plls", "sdr_plls_cu_masked"])
+def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_plls, cu_masked):
     """bench.py's schedule: the stereo/RDS bodies split at the PLL (sdr_*_pre/_pll/_post, or both
     PLLs in one sdr_plls dispatch) on separate streams with the PLLs of block b+1 overlapping block
     b's post part -- identical audio, rds_clean and RDS bits to the one-stream sequential pipeline,
@@ -228,6 +229,17 @@ def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_
     pipe = pkg.Pipeline(nch)
     info = pipe.info
     s_fe, s_pst, s_prd, s_post = (torch.cuda.Stream() for _ in range(4))
+    handles = []
+    if cu_masked:   # bench.py's placement: PLLs on CUs [0, 64) (sdr_stream_create_cu_range), rest elsewhere
+        import ctypes as C
+        L = pkg.lib()
+        L.sdr_stream_create_cu_range.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int]
+        L.sdr_stream_destroy.argtypes = [C.c_void_p]
+        for exclude in (1, 0, 1):
+            h = C.c_void_p()
+            assert L.sdr_stream_create_cu_range(C.byref(h), torch.cuda.current_device(), 0, 64, exclude) == 0
+            handles.append(h.value)
+        s_fe, s_pst, s_post = (torch.cuda.ExternalStream(h) for h in handles)
     ev = lambda: torch.cuda.Event()  # noqa: E731
     pre, pst, prd, post = ([ev() for _ in range(nb)] for _ in range(4))
     lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device="cuda") for _ in range(2)]
@@ -267,6 +279,8 @@ def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_
             got["nbits"].append(pipe.nbits.clone())
         post[b].record(s_post)
     torch.cuda.synchronize()
+    for h in handles:
+        assert pkg.lib().sdr_stream_destroy(C.c_void_p(h)) == 0
     for b in range(nb):
         assert np.array_equal(got["mono"][b].cpu().numpy(), ref["mono"][b]), f"mono block {b}"
         assert np.array_equal(got["stereo"][b].cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
