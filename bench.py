@@ -5,23 +5,29 @@ One step = one block (73 500 I/Q pairs = 30.6 ms of signal) of every channel thr
 reference pipeline of `project 0 r` plus the mono stage: RF front end (u8 I/Q -> FIR /10 ->
 discriminator), mono audio, stereo audio (pilot PLL, mixer, resamplers), RDS DSP (BPF, squaring,
 PLL, mixer, 247/640 resampler, RRC) and RDS bit recovery (cdr, slicer, Manchester, differential).
-Channels are independent and sharded across GPUs (weak scaling: 1024 channels per GPU); inputs are
-synthetic FM multiplex I/Q, generated on the host and resident in HBM before the timed region.
+Channels are independent and sharded across GPUs (weak scaling: 1024 channels per GPU, one process
+per GPU); inputs are synthetic FM multiplex I/Q, 1024 distinct channels per GPU generated on the
+device (synth.TorchMultiplexBatch) and resident in HBM before the timed region.
 
 Three HIP streams per GPU mirror the reference's three threads (project.cpp:134-136): the front end
 produces block b+1 while the stereo and RDS chains consume block b, ordered by events exactly like
-the ThreadSafeQueue protocol (include/threadsafequeue.h:24-74).
+the ThreadSafeQueue protocol (include/threadsafequeue.h:24-74). With N > 1 each block-step's stereo
+audio and RDS bits are gathered to rank 0 over RCCL (xGMI) on a fourth, non-blocking stream.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--no-cpu-baseline]
-For N > 1 launch with torch.distributed.run (one process per GPU, RCCL gather of audio + RDS bits).
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts N ranks itself
+(torch.distributed.run, 127.0.0.1) and exits with their status; the driver may also launch it
+under torch.distributed.run directly.
 """
 from __future__ import annotations
 
 import argparse
+import concurrent.futures as cf
 import json
+import multiprocessing as mp
 import os
 import pathlib
-import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -31,6 +37,8 @@ import numpy as np
 
 ROOT = pathlib.Path(__file__).resolve().parent
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "IQ MSamples/s/node (mono+stereo+RDS), 1/2/4/8 GPU; HBM GB/s %peak"
+VERIFY_CHANNELS = 8             # channels of rank 0 whose outputs are checked after the timed run
 
 
 def _load_pkg():
@@ -46,9 +54,37 @@ def _load_pkg():
     return mod
 
 
-def cu_masked_streams(torch, pkg, dev, spec: str):
+# ------------------------------------------------------------------------------ rank launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv: list[str]) -> int:
+    """bench.py --gpus N (N > 1) without WORLD_SIZE: start N ranks with torch.distributed.run as a
+    CHILD process (never exec: nothing here has touched the GPU, and the ranks must start clean),
+    one per GPU, and return their exit status. Fails if fewer than N GPUs are visible."""
+    if args.backend == "nccl":
+        import torch
+        visible = torch.cuda.device_count()      # does not initialise the GPU on this image
+        if visible < args.gpus:
+            print(f"bench: --gpus {args.gpus} but only {visible} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(pathlib.Path(__file__).resolve()),
+           *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------------ GPU stepper
+def cu_masked_streams(torch, pkg, dev, spec: str, created: list):
     """(fe, pll, post) streams on disjoint CUs through the C ABI (sdr_stream_create_cu_range):
-    the PLL stream on CUs [0, n), the other two on the rest."""
+    the PLL stream on CUs [0, n), the other two on the rest. The runtime creates these streams
+    blocking (hipExtStreamCreateWithCUMask has no flags), so nothing in the timed loop may run on
+    the legacy null stream: the RCCL gather gets its own non-blocking torch stream."""
     import ctypes as C
     n = int(spec)
     L = pkg.lib()
@@ -60,25 +96,22 @@ def cu_masked_streams(torch, pkg, dev, spec: str):
         rc = L.sdr_stream_create_cu_range(C.byref(h), dev.index, 0, n, exclude)
         if rc != 0:
             raise RuntimeError(f"sdr_stream_create_cu_range: {rc} {L.sdr_last_error()}")
-        _MASKED_STREAMS.append(h.value)
+        created.append(h.value)
         out.append(torch.cuda.ExternalStream(h.value, device=dev))
     return tuple(out)
 
 
-_MASKED_STREAMS: list[int] = []
-
-
-def destroy_masked_streams(torch, pkg, dev) -> None:
+def destroy_masked_streams(torch, pkg, dev, created: list) -> None:
     """sdr_stream_destroy the streams cu_masked_streams made (torch does not own them)."""
     import ctypes as C
-    if not _MASKED_STREAMS:
+    if not created:
         return
     torch.cuda.synchronize(dev)
     L = pkg.lib()
     L.sdr_stream_destroy.restype = C.c_int
     L.sdr_stream_destroy.argtypes = [C.c_void_p]
-    while _MASKED_STREAMS:
-        L.sdr_stream_destroy(C.c_void_p(_MASKED_STREAMS.pop()))
+    while created:
+        L.sdr_stream_destroy(C.c_void_p(created.pop()))
 
 
 def _synth_module():
@@ -89,95 +122,298 @@ def _synth_module():
     return mod
 
 
-def _synth_channel(channel: int, nblocks: int) -> np.ndarray:
-    """nblocks consecutive u8 I/Q blocks of one synthetic channel (numpy only, no GPU)."""
+def make_input(torch, nch: int, nblocks: int, first_channel: int, device, kinds=None, seed: int = 0):
+    """[nblocks][nch][2*73500] u8 on the device, nch distinct channels generated there
+    (synth.TorchMultiplexBatch). Rows are padded to a multiple of 16 bytes (147008 for 147000): the
+    front end then stages whole 16-byte I/Q groups."""
     synth = _synth_module()
-    src = synth.FMMultiplexSource(channel)
-    return np.stack([src.next_block() for _ in range(nblocks)])
-
-
-def synth_host_input(nch: int, nblocks: int, first_channel: int) -> np.ndarray:
-    """[nblocks][distinct][2*73500] u8 on the host for min(nch, 16) distinct channels, synthesised in
-    child processes (about 23 ms per channel-block; call before the GPU is initialised)."""
-    import concurrent.futures as cf
-    import multiprocessing as mp
-    distinct = min(nch, 16)
-    workers = max(1, min(distinct, 8, os.cpu_count() or 1))
-    if workers == 1 or nblocks * distinct < 64:
-        chans = [_synth_channel(first_channel + c, nblocks) for c in range(distinct)]
-    else:
-        with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn")) as ex:
-            chans = list(ex.map(_synth_channel, [first_channel + c for c in range(distinct)],
-                                [nblocks] * distinct))
-    return np.ascontiguousarray(np.stack(chans, axis=1))
-
-
-def make_input(torch, nch: int, nblocks: int, first_channel: int, device, host: np.ndarray | None = None):
-    """[nblocks][nch][2*73500] u8 on the device. A few distinct channels are synthesised and tiled
-    across the batch (each channel stays a continuous FM stream across blocks)."""
-    synth = _synth_module()
-    if host is None:
-        host = synth_host_input(nch, nblocks, first_channel)
-    distinct = host.shape[1]
-    # rows padded to a multiple of 16 bytes (147008 for 147000): the front end then stages whole
-    # 16-byte I/Q groups
     row = 2 * synth.BLOCK_IQ
     d = torch.empty((nblocks, nch, (row + 15) // 16 * 16), dtype=torch.uint8, device=device)[:, :, :row]
-    reps = (nch + distinct - 1) // distinct
-    src_t = torch.from_numpy(host).to(device)
-    for r in range(reps):
-        lo, hi = r * distinct, min(nch, (r + 1) * distinct)
-        d[:, lo:hi] = src_t[:, : hi - lo]
+    gen = synth.TorchMultiplexBatch(torch, nch, first_channel, device, kinds=kinds, seed=seed)
+    for b in range(nblocks):
+        gen.next_block(out=d[b])
+    torch.cuda.synchronize(device)
     return d
 
 
-def cpu_baseline(seconds_target: float = 8.0) -> dict | None:
-    """Time the reference's own program (oracle/_ref/project, built from the unmodified sources)
-    in its 3-thread topology on this host, over a bounded sample piped through stdin."""
-    sys.path.insert(0, str(ROOT / "real-time-sdr_amd"))
-    import synth
-    exe = ROOT / "oracle" / "_ref" / "project"
-    nblk_distinct = 32
-    src = synth.FMMultiplexSource(0)
-    blob = b"".join(src.next_block().tobytes() for _ in range(nblk_distinct))
-    samples_per_blob = nblk_distinct * synth.BLOCK_IQ
-    if exe.exists():
-        reps = 150  # 4800 blocks = 353 M I/Q samples (~10 s at the reference's ~37 MS/s)
-        with tempfile.TemporaryFile() as out:
-            t0 = time.perf_counter()
-            p = subprocess.Popen([str(exe), "0", "r"], stdin=subprocess.PIPE, stdout=out, stderr=subprocess.DEVNULL)
+class GpuStepper:
+    """The 1-GPU schedule of one rank: libsdr_amd.so's stage API on three HIP streams."""
+
+    def __init__(self, args, nch: int, first: int, local: int, nblocks: int):
+        import torch
+        self.torch = torch
+        self.pkg = pkg = _load_pkg()
+        self.args, self.nch, self.nblocks = args, nch, nblocks
+        self.dev = dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        self.iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
+        fast = args.numerics == "fast"
+        self.fast = fast
+        self.pipe = pkg.Pipeline(nch, mode=0, rds_on=True, device=local,
+                                 flags=pkg.FLAG_FAST_FRONTEND if fast else 0)
+        self.info = info = self.pipe.info
+        # Three streams, one HIP hardware queue each (GPU_MAX_HW_QUEUES is 4): front end + mono +
+        # the FIRs feeding both PLLs; both PLLs in one dispatch; everything after the PLLs. The
+        # serial PLLs bound the step, so they run back to back across blocks while the other
+        # streams fill the chip. SDR_BENCH_PRIO (A/B): streams (fe, pll, post) at high priority.
+        prio = set(filter(None, os.environ.get("SDR_BENCH_PRIO", "").split(",")))
+        s_fe, s_pll, s_post = (torch.cuda.Stream(dev, priority=-1 if n in prio else 0)
+                               for n in ("fe", "pll", "post"))
+        # SDR_BENCH_CUMASK=<n> (default 64; 0 = no masks): the PLL stream gets CUs [0, n), the
+        # front-end and post streams the complement, so that no other kernel shares a CU's issue
+        # slots with the PLL's lone waves (profiles/r01/ab_cumask.txt).
+        self.created: list[int] = []
+        cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64")
+        if cu_spec not in ("", "0"):
             try:
-                for _ in range(reps):
-                    p.stdin.write(blob)
-                p.stdin.close()
-            except BrokenPipeError:
-                pass
-            p.wait()
-            dt = time.perf_counter() - t0
-        ms = reps * samples_per_blob / dt / 1e6
-        return {"value": round(ms, 3), "unit": "MS/s", "cores": 3, "kind": "reference",
-                "sample": f"reference `project 0 r` (src/*.cpp, g++ -O3, 3 threads RF/audio/RDS) on "
-                          f"{reps * nblk_distinct} blocks = {reps * samples_per_blob / 1e6:.1f} M I/Q samples "
-                          f"of 1 channel via stdin, {dt:.2f} s wall",
-                "host_cpu": _cpu_model(), "nproc": os.cpu_count()}
-    # fallback: the C restatement, one core, full pipeline
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle
-    ch = oracle.Channel(0, True)
-    blocks = [np.frombuffer(blob, np.uint8)[i * 2 * synth.BLOCK_IQ:(i + 1) * 2 * synth.BLOCK_IQ]
-              for i in range(nblk_distinct)]
-    t0 = time.perf_counter()
-    n = 0
-    while time.perf_counter() - t0 < seconds_target:
-        fm = ch.frontend(blocks[n % nblk_distinct])
-        ch.mono(fm)
-        ch.stereo(fm)
-        ch.rds(fm)
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n * synth.BLOCK_IQ / dt / 1e6, 3), "unit": "MS/s", "cores": 1, "kind": "port",
-            "sample": f"oracle C restatement, 1 channel x {n} blocks, 1 thread, {dt:.2f} s",
-            "host_cpu": _cpu_model(), "nproc": os.cpu_count()}
+                s_fe, s_pll, s_post = cu_masked_streams(torch, pkg, dev, cu_spec, self.created)
+            except (RuntimeError, ValueError, AttributeError) as exc:   # plain streams, reported
+                print(f"bench: CU-masked streams unavailable ({exc}); unmasked streams", file=sys.stderr)
+                destroy_masked_streams(torch, pkg, dev, self.created)
+                cu_spec = ""
+        self.cu_spec = cu_spec
+        self.s_fe, self.s_pll, self.s_post = s_fe, s_pll, s_post
+        self.s_gather = torch.cuda.Stream(dev)       # torch pool streams are non-blocking
+        self.mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
+        self.lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]
+        self.bits = [torch.empty(nch, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.clean = torch.empty(nch, info.n_rds, dtype=torch.float32, device=dev)
+        ev = lambda: torch.cuda.Event(enable_timing=False)  # noqa: E731
+        tev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+        self.fe_start, self.fe_end = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
+        self.pll_start, self.pll_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
+        self.pre_done, self.post_done, self.gather_done = ([ev() for _ in range(nblocks)] for _ in range(3))
+        # outputs of a few channels, captured on the producing streams for the check after timing
+        nv = min(VERIFY_CHANNELS, nch)
+        self.vsel = torch.tensor(sorted({int(round(i * (nch - 1) / max(1, nv - 1))) for i in range(nv)}),
+                                 dtype=torch.int64, device=dev)
+        nv = self.vsel.numel()
+        self.cap_mono = torch.empty(nblocks, nv, info.n_audio, dtype=torch.int16, device=dev)
+        self.cap_lr = torch.empty(nblocks, nv, 2 * info.n_audio, dtype=torch.int16, device=dev)
+        self.cap_bits = torch.empty(nblocks, nv, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev)
+        self.cap_nbits = torch.empty(nblocks, nv, dtype=torch.int32, device=dev)
+        self.gathering = False
+
+    def outputs_spec(self):
+        return {"lr": ((self.nch, 2 * self.info.n_audio), self.torch.int16),
+                "bits": ((self.nch, self.pkg.SDR_MAX_BITS), self.torch.uint8)}
+
+    def step(self, b: int, gather=None) -> None:
+        torch, pipe = self.torch, self.pipe
+        s_fe, s_pll, s_post = self.s_fe, self.s_pll, self.s_post
+        # the front end of block b reuses block b-2's parity: both consumers must have released it
+        # (threadsafequeue.h:29-31), i.e. block b-2's post-PLL work is done
+        if b >= 2:
+            s_fe.wait_event(self.post_done[b - 2])
+        self.fe_start[b].record(s_fe)
+        pipe.frontend(self.iq[b], stream=s_fe)                # rffrontend.cpp:58-71
+        self.fe_end[b].record(s_fe)
+        pipe.mono(self.mono, stream=s_fe)                     # mono.cpp:34-42
+        with torch.cuda.stream(s_fe):
+            torch.index_select(self.mono, 0, self.vsel, out=self.cap_mono[b])
+        pipe.stereo_pre(stream=s_fe)                          # stereo.cpp:74, :80
+        pipe.rds_pre(stream=s_fe)                             # rds.cpp:105-116
+        self.pre_done[b].record(s_fe)
+        s_pll.wait_event(self.pre_done[b])
+        self.pll_start[b].record(s_pll)
+        pipe.plls(stream=s_pll)                               # stereo.cpp:77 + rds.cpp:119
+        self.pll_done[b].record(s_pll)
+        s_post.wait_event(self.pll_done[b])
+        if gather is not None and b >= 2:
+            s_post.wait_event(self.gather_done[b - 2])        # lr/bits slot of block b-2 gathered
+        lr, bits = self.lr[b % 2], self.bits[b % 2]
+        pipe.stereo_post(lr, stream=s_post)                   # stereo.cpp:83-107
+        pipe.rds_post(self.clean, bits=True, stream=s_post)   # rds.cpp:122-167
+        with torch.cuda.stream(s_post):
+            bits.copy_(pipe.bits)
+            torch.index_select(lr, 0, self.vsel, out=self.cap_lr[b])
+            torch.index_select(bits, 0, self.vsel, out=self.cap_bits[b])
+            torch.index_select(pipe.nbits, 0, self.vsel, out=self.cap_nbits[b])
+        self.post_done[b].record(s_post)
+        if gather is not None:
+            # final audio / bitstream gather to rank 0 over RCCL (xGMI), on its own non-blocking
+            # stream so that the masked (blocking) streams never meet null-stream work
+            with torch.cuda.stream(self.s_gather):
+                self.s_gather.wait_event(self.post_done[b])
+                gather(lr=lr, bits=bits)
+                self.gather_done[b].record(self.s_gather)
+
+    def synchronize(self) -> None:
+        self.torch.cuda.synchronize(self.dev)
+
+    def report(self, warmup: int, elapsed: float, steps: int) -> dict:
+        """Kernel-level timings of the timed blocks (HIP events on the launching streams)."""
+        info, nch = self.info, self.nch
+        rng = range(warmup, self.nblocks)
+        fe_avg_s = float(np.mean([self.fe_start[b].elapsed_time(self.fe_end[b]) for b in rng])) / 1e3
+        fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
+        pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
+        achieved = fe_bytes / fe_avg_s / 1e9
+        kname = ("k_frontend_mfma" if self.fast else "k_frontend2") + " (u8 I/Q -> 101-tap FIR /10 on I,Q -> FM discriminator)"
+        return {
+            "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": _pmc_traffic(nch, self.args.numerics),
+                         "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4)},
+            "pll": {"kernel": "k_pll: stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial "
+                              "chains in one dispatch",
+                    "bound": "serial recurrence: block_if dependent steps per chain, one lane per chain "
+                             "(per-wave VALU issue, DESIGN.md 4a)",
+                    "avg_launch_ms": round(pll_ms, 4), "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
+                    "share_of_step": round(pll_ms / (elapsed / steps * 1e3), 4)},
+        }
+
+    def isolated_frontend(self) -> dict:
+        """Outside the timed region: the front-end kernel of both numerics modes alone on the GPU
+        (one stream, the same resident inputs), each as a roofline object."""
+        torch, pkg, nch, info = self.torch, self.pkg, self.nch, self.info
+        fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)
+        res = {}
+        for name, flags in (("exact", 0), ("fast", pkg.FLAG_FAST_FRONTEND)):
+            p2 = pkg.Pipeline(nch, mode=0, rds_on=True, device=self.dev.index, flags=flags)
+            s2 = torch.cuda.Stream(self.dev)
+            for b in range(min(self.nblocks, 3)):
+                p2.frontend(self.iq[b], stream=s2)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 20
+            e0.record(s2)
+            for b in range(reps):
+                p2.frontend(self.iq[b % self.nblocks], stream=s2)
+            e1.record(s2)
+            torch.cuda.synchronize(self.dev)
+            ms = e0.elapsed_time(e1) / reps
+            gbs = fe_bytes / (ms / 1e3) / 1e9
+            res[name] = {"kernel": "k_frontend_mfma (int8 MFMA Toeplitz FIR)" if flags else "k_frontend2",
+                         "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(nch, name),
+                         "avg_launch_ms": round(ms, 4)}
+            p2.close()
+        return res
+
+    def captured(self) -> dict:
+        """Host copies of the inputs and captured outputs of the checked channels."""
+        sel = self.vsel.cpu().numpy()
+        iq = self.iq[:, self.vsel].cpu().numpy()            # [nblocks][nv][2*block_iq]
+        return {"channels": [int(c) for c in sel], "iq": iq, "mono": self.cap_mono.cpu().numpy(),
+                "lr": self.cap_lr.cpu().numpy(), "bits": self.cap_bits.cpu().numpy(),
+                "nbits": self.cap_nbits.cpu().numpy()}
+
+    def close(self) -> None:
+        self.pipe.close()
+        destroy_masked_streams(self.torch, self.pkg, self.dev, self.created)
+
+
+def _pmc_traffic(nch: int, numerics: str):
+    """HBM bytes per launch of the front end from rocprofv3 PMC passes (FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE; tools/pmc_summary.py), committed under profiles/."""
+    prof = ROOT / "profiles" / "pmc_frontend.json"
+    try:
+        pm = json.loads(prof.read_text())
+        if pm.get("channels") == nch:
+            return pm.get(numerics, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+# ------------------------------------------------------------------------------ rank path
+def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, backend: str = "nccl") -> dict | None:
+    """One rank of the benchmark: its own channel shard, W warm-up + K timed block-steps bracketed
+    by barrier + synchronize, max over ranks, gather of each block-step's audio and RDS bits to
+    rank 0 (world > 1). Returns the result dict on rank 0 (None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    pkg = _load_pkg()
+    from real_time_sdr_amd.sharding import BlockGather, channel_range, max_over_ranks
+    first, nch = channel_range(args.channels, rank)
+    nblocks = args.warmup + args.steps
+    factory = stepper_factory or GpuStepper
+    st = factory(args, nch, first, local, nblocks)
+    gdev = st.dev if hasattr(st, "dev") else "cpu"
+    bg = None
+    if world > 1 and not args.no_gather:
+        bg = BlockGather(torch, dist, world, st.outputs_spec(), gdev, dst=0)
+    gather = bg.gather if bg is not None else None
+    try:
+        for b in range(args.warmup):
+            st.step(b, gather)
+        st.synchronize()
+        if world > 1:
+            dist.barrier()
+        st.synchronize()
+        t0 = time.perf_counter()
+        for b in range(args.warmup, nblocks):
+            st.step(b, gather)
+        st.synchronize()
+        if world > 1:
+            dist.barrier()
+        st.synchronize()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            elapsed = max_over_ranks(torch, dist, elapsed, gdev)
+        res = None
+        if rank == 0:
+            total_samples = world * nch * st.info.block_iq * args.steps
+            res = {
+                "metric": METRIC,
+                "value": round(total_samples / elapsed / 1e6, 2),
+                "unit": "MS/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "f32",
+                "data": "synthetic FM multiplex I/Q (mono+pilot+stereo+RDS 0A), u8, generated on the device, "
+                        "every channel distinct, resident in HBM",
+                "config": {
+                    "workload": "BASELINE configs[4] per GPU: full mono+stereo+RDS pipeline (project 0 r + mono), "
+                                f"{nch} channels/GPU, mode 0 (2.4 MS/s, 73500 I/Q per block)",
+                    "channels_per_gpu": nch, "channels_total": world * nch, "distinct_channels": world * nch,
+                    "block_iq": st.info.block_iq, "mode": 0,
+                    "pll_cus": (f"PLL stream on CU-mask {st.cu_spec}, other streams on the rest"
+                                if getattr(st, "cu_spec", "") not in ("", "0", None) else "no CU masks"),
+                    "numerics": ("fast: int8 MFMA front end, fm_demod within 1e-5 of the reference, RDS bits "
+                                 "bit-exact" if args.numerics == "fast" else "exact (bit-exact with the reference)"),
+                    "parallelism": f"channel-sharded x{world}" + (
+                        "" if world == 1 or args.no_gather else " + RCCL gather of audio and RDS bits to rank 0"),
+                },
+            }
+            res.update(st.report(args.warmup, elapsed, args.steps))
+            if bg is not None:
+                res["gathered"] = bg.check_last(world)
+            if not args.no_isolated and hasattr(st, "isolated_frontend"):
+                iso = st.isolated_frontend()
+                res["frontend_isolated"] = iso
+                res["roofline_fast"] = iso.get("fast")
+            res["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_leg(args, st.captured())
+            res["verified"] = (res["cpu_baseline"] or {}).get("verified", {}).get("ok")
+        return res
+    finally:
+        if hasattr(st, "close"):
+            st.close()
+        if world > 1:
+            dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------ CPU baseline leg
+def _cpu_share() -> int:
+    """Host cores this run may use: the affinity mask, capped by SDR_BENCH_CPU_CORES (default 16,
+    one GPU's share of the GPU box; nproc there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("SDR_BENCH_CPU_CORES", "16"))))
 
 
 def _cpu_model() -> str:
@@ -190,6 +426,108 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _blob(channel: int, nblocks: int) -> bytes:
+    synth = _synth_module()
+    src = synth.FMMultiplexSource(channel)
+    return b"".join(src.next_block().tobytes() for _ in range(nblocks))
+
+
+def _run_reference(exe, blob: bytes, reps: int) -> float:
+    """Pipe `reps` copies of blob through `project 0 r`; returns the wall seconds."""
+    with tempfile.TemporaryFile() as out:
+        t0 = time.perf_counter()
+        p = subprocess.Popen([str(exe), "0", "r"], stdin=subprocess.PIPE, stdout=out, stderr=subprocess.DEVNULL)
+        try:
+            for _ in range(reps):
+                p.stdin.write(blob)
+            p.stdin.close()
+        except BrokenPipeError:
+            pass
+        p.wait()
+        return time.perf_counter() - t0
+
+
+def _check_channel(job):
+    """Oracle run of one captured channel (the checker; runs in a worker process)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    j, iq, mono, lr, bits, nbits = job
+    ref = oracle.run_channel(iq, 0, True)
+    bad = []
+    for b in range(iq.shape[0]):
+        if not np.array_equal(mono[b], ref["mono"][b]):
+            bad.append(f"mono b{b}")
+        if not np.array_equal(lr[b], ref["stereo"][b]):
+            bad.append(f"stereo b{b}")
+        rb = ref["bits"][b]
+        if rb is None:
+            if int(nbits[b]) != -1:
+                bad.append(f"nbits b{b}")
+        elif int(nbits[b]) != len(rb) or not np.array_equal(bits[b][:len(rb)], rb.astype(np.uint8)):
+            bad.append(f"bits b{b}")
+    return j, bad[:4]
+
+
+def cpu_baseline_leg(args, cap: dict | None) -> dict:
+    """Rank 0 only, outside the timed region: (1) the reference's own program (oracle/_ref/project,
+    built from the unmodified sources) in its 3-thread topology on one channel; (2) the same
+    program on distinct channels concurrently over the host's CPU share (floor(cores/3) processes);
+    (3) the checker: the captured GPU outputs of a few channels compared bit for bit with the
+    oracle run on the same bytes."""
+    synth = _synth_module()
+    exe = ROOT / "oracle" / "_ref" / "project"
+    cores = _cpu_share()
+    res: dict = {"host_cpu": _cpu_model(), "nproc": os.cpu_count(), "cpu_share": cores}
+    if exe.exists():
+        nblk = 32
+        blob = _blob(0, nblk)
+        reps = 150  # 4800 blocks = 353 M I/Q samples (~10 s at the reference's ~37 MS/s)
+        dt = _run_reference(exe, blob, reps)
+        res.update({"value": round(reps * nblk * synth.BLOCK_IQ / dt / 1e6, 3), "unit": "MS/s", "cores": 3,
+                    "kind": "reference",
+                    "sample": f"reference `project 0 r` (src/*.cpp, g++ -O3, 3 threads RF/audio/RDS) on "
+                              f"{reps * nblk} blocks = {reps * nblk * synth.BLOCK_IQ / 1e6:.1f} M I/Q samples of "
+                              f"1 channel via stdin, {dt:.2f} s wall"})
+        nproc = max(1, cores // 3)
+        nb2, reps2 = 8, 400                  # per process: 3200 blocks of its own channel
+        blobs = [_blob(1 + i, nb2) for i in range(nproc)]
+        with cf.ThreadPoolExecutor(nproc) as ex:
+            t0 = time.perf_counter()
+            list(ex.map(lambda bl: _run_reference(exe, bl, reps2), blobs))
+            dt2 = time.perf_counter() - t0
+        res["all_cores"] = {"value": round(nproc * reps2 * nb2 * synth.BLOCK_IQ / dt2 / 1e6, 3), "unit": "MS/s",
+                            "cores": 3 * nproc, "kind": "reference",
+                            "sample": f"{nproc} concurrent `project 0 r` processes x 3 threads, distinct channels, "
+                                      f"{reps2 * nb2} blocks each, {dt2:.2f} s wall"}
+    else:
+        # the C restatement, one core, full pipeline (this tree built without /root/reference)
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+        blocks = np.frombuffer(_blob(0, 8), np.uint8).reshape(8, -1)
+        ch = oracle.Channel(0, True)
+        t0, n = time.perf_counter(), 0
+        while time.perf_counter() - t0 < 8.0:
+            fm = ch.frontend(blocks[n % 8])
+            ch.mono(fm)
+            ch.stereo(fm)
+            ch.rds(fm)
+            n += 1
+        dt = time.perf_counter() - t0
+        res.update({"value": round(n * synth.BLOCK_IQ / dt / 1e6, 3), "unit": "MS/s", "cores": 1, "kind": "port",
+                    "sample": f"oracle C restatement, 1 channel x {n} blocks, 1 thread, {dt:.2f} s"})
+    if cap is not None:
+        jobs = [(j, cap["iq"][:, j], cap["mono"][:, j], cap["lr"][:, j], cap["bits"][:, j], cap["nbits"][:, j])
+                for j in range(len(cap["channels"]))]
+        with cf.ProcessPoolExecutor(min(len(jobs), cores), mp_context=mp.get_context("spawn")) as ex:
+            results = dict(ex.map(_check_channel, jobs))
+        bad = {cap["channels"][j]: v for j, v in results.items() if v}
+        res["verified"] = {"ok": not bad, "channels": cap["channels"], "blocks": int(cap["iq"].shape[0]),
+                           "outputs": "mono int16, stereo int16, RDS bits (every block incl. warm-up), "
+                                      "bit for bit against the oracle on the same input bytes",
+                           "mismatches": bad or None}
+    return res
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,216 +537,22 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL gather (N>1)")
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated front-end timings")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl", help=argparse.SUPPRESS)
     ap.add_argument("--numerics", choices=("exact", "fast"), default="exact",
                     help="exact: every output bit-identical to the reference; fast: the matrix-core front end "
                          "(fm_demod within 1e-5, RDS bits bit-exact)")
-    args = ap.parse_args()
-
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    nblocks = args.warmup + args.steps
-    # this rank's synthetic input, made in child processes before anything touches the GPU
-    host_iq = synth_host_input(args.channels, nblocks, first_channel=rank * args.channels)
-
-    import torch
-    import torch.distributed as dist
-
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    pkg = _load_pkg()
-
-    from real_time_sdr_amd.sharding import channel_range
-    first, nch = channel_range(args.channels, rank)
-    assert first == rank * args.channels
-    iq = make_input(torch, nch, nblocks, first_channel=first, device=dev, host=host_iq)
-    del host_iq
-    fast = args.numerics == "fast"
-    pipe = pkg.Pipeline(nch, mode=0, rds_on=True, device=local, flags=pkg.FLAG_FAST_FRONTEND if fast else 0)
-    info = pipe.info
-    # Three streams, one HIP hardware queue each (GPU_MAX_HW_QUEUES is 4 and one serves the null
-    # stream; a fourth stream would share a queue and serialise behind it): front end + mono + the
-    # FIRs feeding both PLLs; both PLLs in one dispatch; everything after the PLLs. The serial PLLs
-    # bound the step, so they run back to back across blocks while the other streams fill the chip.
-    # SDR_BENCH_PRIO (A/B): comma list of streams (fe, pll, post) created with high priority
-    prio = set(filter(None, os.environ.get("SDR_BENCH_PRIO", "").split(",")))
-    s_fe, s_pll, s_post = (torch.cuda.Stream(dev, priority=-1 if n in prio else 0) for n in ("fe", "pll", "post"))
-    # SDR_BENCH_CUMASK=<n> (default 64; 0 = no masks): the PLL stream gets CUs [0, n) of its
-    # own, the front-end and post streams the complement,
-    # so that no other kernel shares a CU's issue slots with the PLL's 32 lone waves. Measured
-    # (profiles/r01/ab_cumask.txt): none 0.895 ms/step, 8 CUs 1.86, 16 0.99, 32 0.871, 48-96
-    # 0.864-0.870, 128 0.911 (front end starved)
-    cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64")
-    if cu_spec not in ("", "0"):
-        try:
-            s_fe, s_pll, s_post = cu_masked_streams(torch, pkg, dev, cu_spec)
-        except (RuntimeError, ValueError, AttributeError) as exc:   # plain streams, reported
-            print(f"bench: CU-masked streams unavailable ({exc}); unmasked streams", file=sys.stderr)
-            destroy_masked_streams(torch, pkg, dev)
-            cu_spec = ""
-    mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
-    lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]
-    bits = [torch.empty(nch, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev) for _ in range(2)]
-    clean = torch.empty(nch, info.n_rds, dtype=torch.float32, device=dev)
-    ev = lambda: torch.cuda.Event(enable_timing=False)  # noqa: E731
-    fe_start = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
-    fe_end = [torch.cuda.Event(enable_timing=True) for _ in range(nblocks)]
-    # SDR_BENCH_PLL_TIMING=0 (A/B): no timestamp packets on the PLL stream (pll object omitted)
-    pll_timing = os.environ.get("SDR_BENCH_PLL_TIMING", "1") != "0"
-    pll_start = [torch.cuda.Event(enable_timing=pll_timing) for _ in range(nblocks)]
-    pre_done, post_done, gather_done = ([ev() for _ in range(nblocks)] for _ in range(3))
-    pll_done = [torch.cuda.Event(enable_timing=pll_timing) for _ in range(nblocks)]
-    gather = None
-    if world > 1 and not args.no_gather:
-        from real_time_sdr_amd.sharding import BlockGather
-        gather = BlockGather(torch, dist, world, {"lr": ((nch, 2 * info.n_audio), torch.int16),
-                                                  "bits": ((nch, pkg.SDR_MAX_BITS), torch.uint8)}, dev)
-
-    def step(b: int) -> None:
-        # the front end of block b reuses block b-2's parity: both consumers must have released it
-        # (threadsafequeue.h:29-31), i.e. block b-2's post-PLL work is done
-        if b >= 2:
-            s_fe.wait_event(post_done[b - 2])
-        fe_start[b].record(s_fe)
-        pipe.frontend(iq[b], stream=s_fe)                # rffrontend.cpp:58-71
-        fe_end[b].record(s_fe)
-        pipe.mono(mono, stream=s_fe)                     # mono.cpp:34-42
-        pipe.stereo_pre(stream=s_fe)                     # stereo.cpp:74, :80
-        pipe.rds_pre(stream=s_fe)                        # rds.cpp:105-116
-        pre_done[b].record(s_fe)
-        s_pll.wait_event(pre_done[b])
-        pll_start[b].record(s_pll)
-        pipe.plls(stream=s_pll)                          # stereo.cpp:77 + rds.cpp:119
-        pll_done[b].record(s_pll)
-        s_post.wait_event(pll_done[b])
-        if gather is not None and b >= 2:
-            s_post.wait_event(gather_done[b - 2])        # lr/bits slot of block b-2 gathered
-        pipe.stereo_post(lr[b % 2], stream=s_post)       # stereo.cpp:83-107
-        pipe.rds_post(clean, bits=True, stream=s_post)   # rds.cpp:122-167
-        with torch.cuda.stream(s_post):
-            bits[b % 2].copy_(pipe.bits)
-        post_done[b].record(s_post)
-        if gather is not None:
-            # final audio / bitstream gather over RCCL (xGMI)
-            cur = torch.cuda.current_stream(dev)
-            cur.wait_event(post_done[b])
-            gather.gather(lr=lr[b % 2], bits=bits[b % 2])
-            gather_done[b].record(cur)
-
-    for b in range(args.warmup):
-        step(b)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for b in range(args.warmup, nblocks):
-        step(b)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        from real_time_sdr_amd.sharding import max_over_ranks
-        elapsed = max_over_ranks(torch, dist, elapsed, dev)
-
-    # front-end kernel (FIR /10 + discriminator) duration from HIP events on its own stream
-    fe_ms = [fe_start[b].elapsed_time(fe_end[b]) for b in range(args.warmup, nblocks)]
-    fe_avg_s = float(np.mean(fe_ms)) / 1e3
-    fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
-    achieved = fe_bytes / fe_avg_s / 1e9
-    # the serial PLL dispatch (both PLLs of a block) that bounds the block-step
-    pll_ms = (float(np.mean([pll_start[b].elapsed_time(pll_done[b]) for b in range(args.warmup, nblocks)]))
-              if pll_timing else float("nan"))
-    total_samples = world * nch * info.block_iq * args.steps
-    value = total_samples / elapsed / 1e6
-
-    # informational, outside the timed region: the front-end kernel of both numerics modes alone
-    # on the GPU (one stream, the same resident inputs), for comparison with the in-pipeline figure
-    isolated = {}
-    if rank == 0 and not args.no_isolated:
-        for name, flags in (("exact", 0), ("fast", pkg.FLAG_FAST_FRONTEND)):
-            p2 = pkg.Pipeline(nch, mode=0, rds_on=True, device=local, flags=flags)
-            s2 = torch.cuda.Stream(dev)
-            for b in range(min(nblocks, 3)):
-                p2.frontend(iq[b], stream=s2)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            reps = 20
-            e0.record(s2)
-            for b in range(reps):
-                p2.frontend(iq[b % nblocks], stream=s2)
-            e1.record(s2)
-            torch.cuda.synchronize(dev)
-            ms = e0.elapsed_time(e1) / reps
-            gbs = fe_bytes / (ms / 1e3) / 1e9
-            isolated[name] = {"avg_launch_ms": round(ms, 4), "achieved_GBps": round(gbs, 1),
-                              "frac": round(gbs / HBM_PEAK_GBS, 4)}
-            p2.close()
-
-    if rank == 0:
-        # HBM bytes per launch of the same kernel from rocprofv3 PMC passes (FETCH_SIZE x2 gfx950
-        # correction + WRITE_SIZE; tools/pmc_summary.py), committed under profiles/
-        prof = ROOT / "profiles" / "pmc_frontend.json"
-        traffic = None
-        if prof.exists():
-            try:
-                pm = json.loads(prof.read_text())
-                if pm.get("channels") == nch:
-                    traffic = pm.get(args.numerics, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        res = {
-            "metric": "IQ MSamples/s/node (mono+stereo+RDS), 1/2/4/8 GPU; HBM GB/s %peak",
-            "value": round(value, 2),
-            "unit": "MS/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic FM multiplex I/Q (mono+pilot+stereo+RDS 0A), u8, resident in HBM",
-            "config": {
-                "workload": "BASELINE configs[4] per GPU: full mono+stereo+RDS pipeline (project 0 r + mono), "
-                            f"{nch} channels/GPU, mode 0 (2.4 MS/s, 73500 I/Q per block)",
-                "channels_per_gpu": nch, "channels_total": world * nch, "block_iq": info.block_iq,
-                "mode": 0,
-                "pll_cus": (f"PLL stream on CU-mask {cu_spec}, other streams on the rest"
-                            if cu_spec not in ("", "0") else "no CU masks"),
-                "numerics": ("fast: int8 MFMA front end, fm_demod within 1e-5 of the reference, RDS bits bit-exact"
-                             if fast else "exact (bit-exact with the reference)"),
-                "parallelism": f"channel-sharded x{world}" + ("" if world == 1 or args.no_gather else " + RCCL all-gather"),
-            },
-            "roofline": {
-                "kernel": ("k_frontend_mfma" if fast else "k_frontend2") +
-                          " (u8 I/Q -> 101-tap FIR /10 on I,Q -> FM discriminator)",
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4),
-            },
-            "frontend_isolated": isolated or None,
-            "pll": {
-                "kernel": "k_pll: stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial "
-                          "chains in one dispatch",
-                "bound": "serial recurrence: block_if dependent steps per chain, one lane per chain "
-                         "(per-wave VALU issue and latency, DESIGN.md 4a)",
-                "avg_launch_ms": round(pll_ms, 4),
-                "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
-                "share_of_step": round(pll_ms / (elapsed / args.steps * 1e3), 4),
-            },
-            "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline(),
-        }
-        print(json.dumps(res))
-    pipe.close()
-    destroy_masked_streams(torch, pkg, dev)
-    if world > 1:
-        dist.destroy_process_group()
+    if world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} (--gpus {args.gpus}); measuring {world} rank(s)", file=sys.stderr)
+    res = run_rank(args, world, rank, local)
+    if res is not None:
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":
