@@ -457,6 +457,71 @@ PLLM_HD void dd_sincos(double t, double* s_out, double* c_out) {
     *s_out = s.hi;
 }
 
+// 2/pi in 24-bit chunks: chunk k holds bits 24k+1 .. 24k+24 after the binary point
+// (tools/pllmath/dd_consts.py, from pi in exact rational arithmetic)
+constexpr uint32_t IPIO2_24[16] = {
+    0xA2F983, 0x6E4E44, 0x1529FC, 0x2757D1, 0xF534DD, 0xC0DB62, 0x95993C, 0x439041,
+    0xFE5163, 0xABDEBB, 0xC561B7, 0x246E3A, 0x424DD2, 0xE00649, 0x2EEA09, 0xD1921C};
+
+// Payne-Hanek reduction of a finite f32 |t| >= 2^30: t = M 2^E with M < 2^24 an integer, so
+// t (2/pi) = sum_k M c_k 2^(E - 24(k+1)), every product M c_k < 2^48 exact in f64. Terms whose
+// scale makes them multiples of 4 drop out (only t (2/pi) mod 4 matters), the leading kept terms
+// are reduced mod 4 exactly, the rest down to 2^-120 are summed in double-double. Returns the
+// quadrant q (mod 4) and r = (t (2/pi) - q) pi/2 in double-double, |r| <= pi/4 (+2^-100); the
+// reduction error is below 2^-110 absolute (the closest f32 to a multiple of pi/2 is ~2^-30 away,
+// so r keeps > 2^-80 relative accuracy: RN64 of cos/sin stays exact).
+PLLM_HD int dd_reduce_f32_large(float t, DD& r) {
+    const uint32_t bits = __builtin_bit_cast(uint32_t, t) & 0x7FFFFFFFu;
+    const int E = (int)(bits >> 23) - 127 - 23;
+    const double M = (double)((bits & 0x7FFFFFu) | 0x800000u);
+    DD acc = {0.0, 0.0};
+    for (int k = 0; k < 16; k++) {
+        const int s = E - 24 * (k + 1);              // term = (M c_k) 2^s
+        if (s >= 2) continue;                        // a multiple of 4
+        if (s + 48 < -120) break;                    // below 2^-120 (and every later term)
+        double p = M * (double)IPIO2_24[k];          // exact, < 2^48
+        if (s > -48) {                               // p 2^s may reach 4: keep p mod 2^(2-s)
+            const double m = __builtin_ldexp(1.0, 2 - s);
+            p = p - __builtin_floor(p / m) * m;      // exact (power-of-two modulus)
+        }
+        acc = dd_add(acc, DD{__builtin_ldexp(p, s), 0.0});
+    }
+    double q = __builtin_rint(acc.hi);
+    DD f = dd_add(acc, DD{-q, 0.0});
+    if (f.hi > 0.5) { f = dd_add(f, DD{-1.0, 0.0}); q += 1.0; }
+    if (f.hi < -0.5) { f = dd_add(f, DD{1.0, 0.0}); q -= 1.0; }
+    r = dd_mul(f, DD{DD_PIO2_HI, DD_PIO2_LO});
+    int qi = (int)q & 3;
+    if (t < 0.0f) {                                  // t = -|t|: negate r and q
+        r = dd_neg(r);
+        qi = (4 - qi) & 3;
+    }
+    return qi;
+}
+
+// RN64(cos t), RN64(sin t) for any finite f32 t (glibc's sin/cos of pll.cpp:49-50 and :52 for
+// arguments beyond the Cody-Waite range of dd_sincos_dd as well)
+PLLM_HD void dd_sincos_f32(float t, double* s_out, double* c_out) {
+    if (__builtin_fabs(t) < 0x1p30f) {
+        dd_sincos((double)t, s_out, c_out);
+        return;
+    }
+    DD r;
+    const int q = dd_reduce_f32_large(t, r);
+    const DD z = dd_mul(r, r);
+    const DD cr = dd_trig_series(z, 0);
+    const DD sr = dd_mul(dd_trig_series(z, 1), r);
+    double c, s;
+    switch (q) {                                     // cos t + i sin t = i^q (cos r + i sin r)
+        case 0: c = cr.hi; s = sr.hi; break;
+        case 1: c = -sr.hi; s = cr.hi; break;
+        case 2: c = -cr.hi; s = -sr.hi; break;
+        default: c = sr.hi; s = -cr.hi; break;
+    }
+    *c_out = c;
+    *s_out = s;
+}
+
 // RN64(atan2(y, x)) (glibc's atan2 of pll.cpp:39) for f32 inputs. th0 is any approximation within a
 // few ulps (the device libm's); rotating (x, y) by -th0 in double-double leaves a residual angle
 // |d| < 2^-48, and atan2(y, x) = th0 + d - d^3/3 to 2^-140. Zeros, infinities and NaN return th0:

@@ -1160,33 +1160,38 @@ __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
 //     and |e| < pi - 2^-30 (so the wrap to [-pi, pi] is the reference's),
 //   * every cos/sin is at least 64 f64 ulps from an f32 tie (tie),
 //   * the chunk ends with |phaseEst| < 2^28, |integrator| < 2^20 (finite: a NaN or inf from an
-//     invalid input -- pll_rx gives NaN for |x| < 2^-60 -- propagates into both) and
-//     |w| (|toff| + CHUNK) < 2^29, which bounds every |t| of the chunk below 2^30 (T_MAX).
+//     invalid input -- pll_rx gives NaN for |x| < 2^-60 -- propagates into both),
+//   * every |t| of the chunk is below 2^30 (T_MAX, the two-fma reduction's range): with the trigArg
+//     table (TAB) the launch checked |w| (|toff| + n + 1) < 1.375 * 2^29, which leaves room for
+//     |phaseEst| < 2^28 plus 16 steps of drift; without it the chunk's largest |t| is tracked.
 struct PllProof {
     double emax = 0.0;
     uint32_t split = 0u;
     uint32_t tie = ~0u;
+    float tmax = 0.0f;
 };
+constexpr double PLL_TAB_WT_MAX = 0x1.6p29;   // |w * trigOffset| bound of the table path (above)
 
 // TAB: the trigArg offsets come from a table whose range the kernel checked once (pll_run)
 template <bool TAB>
 __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
     return (pf.emax < pllm::PI - 0x1p-30) & (pf.split == 0u) & (pf.tie > pllm::TIE_MIN) &
            (__builtin_fabs(r.ph) < 0x1p28f) & (__builtin_fabs(r.integ) < 0x1p20f) &
-           (TAB || (__builtin_fabs(w) * (__builtin_fabs(r.toff) + (double)chunk) < 0x1p29));
+           (TAB || (pf.tmax < 0x1p30f));
 }
 
 // the f64 libm results of the reference step (pll.cpp:39, :49-50), out of line: only the rare
 // fallbacks call them, and the unrolled redo chunks stay small. They return glibc's value RN64(f)
 // from double-double evaluations (pll_math.h), not the device libm's, which differs from glibc by
 // 1-2 ulps on 3-27% of inputs -- enough to flip an f32 rounding on the near-midpoint inputs that
-// reach a fallback. |t| >= 2^30 (beyond the reduction) keeps the device libm.
+// reach a fallback. |t| >= 2^30 (a stream past ~25 min for the 114 kHz PLL) reduces by
+// Payne-Hanek in double-double (pll_math.h dd_reduce_f32_large); only inf/NaN keep the device libm.
 __device__ __noinline__ float pll_atan2_ref(float eQ, float eI) {
     return (float)pllm::dd_atan2_f32(eQ, eI, atan2((double)eQ, (double)eI));
 }
 __device__ __noinline__ void pll_sincos_ref(float t, double* s, double* c) {
-    if (__builtin_fabs(t) < 0x1p30f)
-        pllm::dd_sincos((double)t, s, c);
+    if (__builtin_fabs(t) <= 3.4028234663852886e38f)
+        pllm::dd_sincos_f32(t, s, c);
     else
         sincos((double)t, s, c);
 }
@@ -1242,6 +1247,7 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
         pf.emax = fmax(pf.emax, __builtin_fabs(p.e));
         pf.split |= p.split;
         pf.tie = min(pf.tie, sc.tie);
+        if (!TAB) pf.tmax = fmaxf(pf.tmax, __builtin_fabsf(t));
     }
     t_out = t;
 }
@@ -1385,7 +1391,7 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
     // |phaseEst| < 2^28). All 64 lanes build it, then the lanes without a channel leave.
     const double toff_l0 = __shfl(toff0, 0);
     const bool tab = tab_ok && __all(!active || toff0 == toff_l0) &&
-                     __builtin_fabs(w) * (__builtin_fabs(toff_l0) + (double)n + 1.0) < 0x1p29;
+                     __builtin_fabs(w) * (__builtin_fabs(toff_l0) + (double)n + 1.0) < PLL_TAB_WT_MAX;
     if (tab) {
         for (int k = threadIdx.x; k < n; k += 64) wtab[k] = w * (toff_l0 + (double)(k + 1));   // pll.cpp:46-47
         __syncthreads();

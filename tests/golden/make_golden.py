@@ -13,8 +13,11 @@ stored) and the outputs are what the reference computes on them.
   project_e2e.json        the real reference program `project 0 m|s|r` on channel 0's input:
                           SHA-256 of its stdout PCM (whole blocks) and its RDS stderr text,
                           which pins the stage glue of oracle/ref_harness.cpp
+  golden_modes123.json    modes 1-3 (project.cpp:76-103: 1.44 / 2.4 / 1.152 MS/s front ends, the
+                          147/800 and 147/1280 audio resamplers), channel 7, 7 blocks each: per-block
+                          SHA-256 of every output, cdr offsets, symbols and bits
 
-usage: python tests/golden/make_golden.py
+usage: python tests/golden/make_golden.py [--modes-only]
 """
 from __future__ import annotations
 
@@ -82,8 +85,49 @@ def run_harness(iq: np.ndarray, tmp: pathlib.Path, tag: str, dump=DUMP_BLOCKS) -
     return out
 
 
+MODES_CHANNEL = 7
+MODES_NBLOCKS = 7
+
+
+def make_modes(tmp: pathlib.Path) -> dict:
+    """golden_modes123.json: the reference harness in modes 1-3 on channel 7's input."""
+    fix = {"channel": MODES_CHANNEL, "nblocks": MODES_NBLOCKS, "modes": {}}
+    for mode in (1, 2, 3):
+        U, D, decim = {1: (1, 9, 4), 2: (147, 800, 10), 3: (147, 1280, 3)}[mode]
+        block_iq = (1470 * decim * D) // U
+        src = synth.FMMultiplexSource(MODES_CHANNEL)
+        iq = np.stack([src.next_block(block_iq) for _ in range(MODES_NBLOCKS)])
+        inp = tmp / f"m{mode}.u8"
+        iq.tofile(inp)
+        pre = str(tmp / f"m{mode}_")
+        subprocess.run([str(REF / "ref_harness"), str(inp), str(MODES_NBLOCKS), str(mode), "1", pre], check=True)
+        nb = MODES_NBLOCKS
+        outs = {"fm_demod": np.fromfile(pre + "fm_demod.f32", np.float32).reshape(nb, -1),
+                "mono": np.fromfile(pre + "mono.i16", np.int16).reshape(nb, -1),
+                "stereo": np.fromfile(pre + "stereo.i16", np.int16).reshape(nb, -1),
+                "rds_clean": np.fromfile(pre + "rds_clean.f32", np.float32).reshape(nb, -1)}
+        blocks = []
+        for i, line in enumerate(open(pre + "bits.txt").read().splitlines()):
+            p = line.split()
+            b = {"block": int(p[0])}
+            if len(p) > 1:
+                b.update({"offset": int(p[1]), "symbols": p[2], "bits": p[3]})
+            b.update({k + "_sha256": sha(v[i]) for k, v in outs.items()})
+            blocks.append(b)
+        fix["modes"][str(mode)] = {"block_iq": block_iq, "input_sha256": sha(iq),
+                                   "lengths": {k: int(v.shape[1]) for k, v in outs.items()},
+                                   "blocks": blocks}
+    return fix
+
+
 def main() -> None:
     subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref", "oracle"], check=True)
+    if "--modes-only" in sys.argv:
+        with tempfile.TemporaryDirectory() as td:
+            fix = make_modes(pathlib.Path(td))
+        (GOLD / "golden_modes123.json").write_text(json.dumps(fix, indent=0) + "\n")
+        print("wrote golden_modes123.json")
+        return
     npz: dict[str, np.ndarray] = {}
     long_fix: dict = {"channels": {}, "nblocks": N_LONG, "mode": 0}
     with tempfile.TemporaryDirectory() as td:
@@ -131,6 +175,7 @@ def main() -> None:
                               "stderr": r.stderr.decode()}
                 assert e2e["r"]["stderr"] == short["rds_text"], "RDS text of project 0 r != harness"
                 (GOLD / "project_e2e.json").write_text(json.dumps(e2e, indent=1) + "\n")
+        (GOLD / "golden_modes123.json").write_text(json.dumps(make_modes(tmp), indent=0) + "\n")
     np.savez_compressed(GOLD / "golden_mode0.npz", **npz)
     (GOLD / "golden_mode0_long.json").write_text(json.dumps(long_fix, indent=0) + "\n")
     print("wrote", sorted(p.name for p in GOLD.iterdir()))

@@ -120,6 +120,16 @@ def test_other_modes_vs_oracle(pkg, synth, oracle, torch_cuda, mode):
     iq = np.stack([src.next_block(ch.block_iq) for _ in range(nb)])
     out = _run_pipeline(pkg, torch_cuda, [iq], nb, mode=mode)
     ref = oracle.run_channel(iq, mode, True)
+    # pinned to the unmodified reference (tests/golden/golden_modes123.json)
+    import json
+    from conftest import GOLD
+    fix = json.loads((GOLD / "golden_modes123.json").read_text())["modes"][str(mode)]
+    assert sha(iq) == fix["input_sha256"]
+    for b, want in enumerate(fix["blocks"]):
+        for k, key in (("fm", "fm_demod"), ("mono", "mono"), ("stereo", "stereo"), ("clean", "rds_clean")):
+            assert sha(out[k][b][0]) == want[key + "_sha256"], f"mode {mode} {key} block {b} vs reference"
+        if "bits" in want:
+            assert _bitstr(out["bits"][b][0], int(out["nbits"][b][0])) == want["bits"], f"mode {mode} bits {b}"
     for b in range(nb):
         assert np.array_equal(out["fm"][b][0].view(np.uint32), ref["fm_demod"][b].view(np.uint32)), f"fm b{b}"
         assert np.array_equal(out["mono"][b][0], ref["mono"][b]), f"mono b{b}"
@@ -289,3 +299,36 @@ def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_
         assert np.array_equal(got["nbits"][b].cpu().numpy(), ref["nbits"][b]), f"nbits block {b}"
         assert np.array_equal(got["bits"][b].cpu().numpy(), ref["bits"][b]), f"bits block {b}"
     pipe.close()
+
+
+@pytest.mark.parametrize("row_align", [1, 16], ids=["rows_8B_aligned", "rows_16B_aligned"])
+def test_fast_frontend_all_outputs_tolerance(pkg, synth, golden_long, oracle, torch_cuda, row_align):
+    """SDR_FLAG_FAST_FRONTEND over the 200-block golden run (2 channels, 6.1 s, PLL phases past
+    2^21 rad): every output against the oracle with the north-star tolerance. Floats (fm_demod,
+    rds_clean): max |got - ref| <= 1e-5 * max |ref| per block. int16 audio (mono, stereo):
+    short(16384 y) of a y within 1e-5 relative moves by at most 16384 * 1e-5 * max|y| < 1 before the
+    truncation, so the allowance is 1 LSB per sample; RDS bits bit-exact (mono.cpp:40-42,
+    stereo.cpp:100-107, rds.cpp:157-167)."""
+    nb = golden_long["nblocks"]
+    chans = [int(c) for c in golden_long["channels"]]
+    iqs = [channel_input(synth, c, nb, golden_long["channels"][str(c)]["input_sha256"]) for c in chans]
+    out = _run_pipeline(pkg, torch_cuda, iqs, nb, flags=pkg.FLAG_FAST_FRONTEND, row_align=row_align)
+    worst = {k: 0.0 for k in ("fm", "clean", "mono", "stereo")}
+    for j, c in enumerate(chans):
+        ref = oracle.run_channel(iqs[j], 0, True)
+        for b in range(nb):
+            for k, key in (("fm", "fm_demod"), ("clean", "rds_clean")):
+                got, want = out[k][b][j].astype(np.float64), ref[key][b].astype(np.float64)
+                rel = np.max(np.abs(got - want)) / max(np.max(np.abs(want)), 1e-30)
+                worst[k] = max(worst[k], rel)
+                assert rel <= 1e-5, f"{key} ch{c} block {b}: {rel:.2e} relative"
+            for k, key in (("mono", "mono"), ("stereo", "stereo")):
+                d = np.max(np.abs(out[k][b][j].astype(np.int32) - ref[key][b].astype(np.int32)))
+                worst[k] = max(worst[k], float(d))
+                assert d <= 1, f"{key} ch{c} block {b}: {d} LSB"
+            if ref["bits"][b] is not None:
+                assert _bitstr(out["bits"][b][j], int(out["nbits"][b][j])) == _bitstr(ref["bits"][b], len(ref["bits"][b])), \
+                    f"bits ch{c} block {b}"
+            else:
+                assert int(out["nbits"][b][j]) == -1
+    print("fast front end, worst over 200 blocks x 2 channels:", worst)

@@ -184,3 +184,68 @@ def test_fmpll_full_width(pkg, oracle, torch_cuda, freq, nco, bw):
             if not np.array_equal(_u32(out[c]), _u32(out_ref[c])):
                 bad.append(c)
         assert not bad, f"block {blk}: {len(bad)} channels differ, first {bad[:8]}"
+
+
+@pytest.mark.parametrize("freq,nco,bw", [(19e3, 2.0, 0.01), (114e3, 0.5, 0.001)])
+def test_fmpll_long_stream(pkg, oracle, torch_cuda, freq, nco, bw):
+    """Hours into a stream: trigOffset from 2e8 to 1.5e9 samples (pll.cpp:46-47), so trigArg passes
+    the table bound (|w toff| < 1.375 * 2^29), the two-fma reduction's 2^30 (25 min for the 114 kHz
+    PLL) and 2^32; past 2^30 every cos/sin is the Payne-Hanek double-double fallback (glibc's f64
+    value), and the NCO's cos(t * ncoScale) with it. Two blocks, bit-exact against the oracle,
+    outputs and state (the first block starts from feedback that does not match trigArg)."""
+    torch = torch_cuda
+    n = 7350
+    toffs = [2.0e8, 2.6e8, 3.55e8, 3.6e8, 4.0e8, 7.2e8, 1.5e9, 1.5e9 + 7.0]
+    nch = len(toffs)
+    arr = (pkg.PllState * nch)()
+    refs = []
+    for i, to in enumerate(toffs):
+        arr[i] = pkg.PllState(1.0, 0.0, 1e-5, 0.25, to, 1.0)
+        refs.append(oracle.PllState(1.0, 0.0, 1e-5, 0.25, to, 1.0))
+    d_st = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).cuda()
+    out_ref = [np.zeros(n + 1, np.float32) for _ in range(nch)]
+    for o in out_ref:
+        o[-1] = 1.0
+    rng = np.random.default_rng(23)
+    for blk in range(2):
+        t = (np.arange(n) + blk * n) / 240000.0
+        x = np.stack([(0.1 * np.cos(2 * np.pi * (freq + 1.5 * c) * t + 0.4 * c)
+                       + 0.01 * rng.standard_normal(n)).astype(np.float32) for c in range(nch)])
+        d_out = torch.zeros(nch, n + 1, device="cuda")
+        pkg.fmpll(d_out, torch.from_numpy(x).cuda(), freq, 240000.0, d_st, nco, 0.0, bw)
+        out = d_out.cpu().numpy()
+        got = pkg.pll_state_from_tensor(d_st)
+        for c in range(nch):
+            oracle.fmpll(x[c], freq, 240000.0, out_ref[c], refs[c], nco, 0.0, bw)
+            assert np.array_equal(_u32(out[c]), _u32(out_ref[c])), f"toff {toffs[c]:g} block {blk}"
+            for f in ("feedbackI", "feedbackQ", "integrator", "phaseEst", "trigOffset", "lastCarrier"):
+                assert getattr(got[c], f) == getattr(refs[c], f), f"toff {toffs[c]:g} block {blk} {f}"
+
+
+def test_fmpll_long_stream_shared_offset(pkg, oracle, torch_cuda):
+    """64 channels sharing trigOffset just below and just above the trigArg-table bound of the
+    114 kHz PLL (the context path of a long-running receiver): bit-exact against the oracle."""
+    torch = torch_cuda
+    n, freq, nco, bw = 7350, 114e3, 0.5, 0.001
+    w = 2 * np.pi * np.float32(freq / 240000.0)
+    for toff in (float(int(0x1.6p29 / w) - n - 2), float(int(0x1.6p29 / w) + 5)):
+        nch = 64
+        d_st = pkg.pll_state_tensor(nch)
+        arr = (pkg.PllState * nch)()
+        refs = []
+        for i in range(nch):
+            arr[i] = pkg.PllState(1.0, 0.0, 0.0, 0.0, toff, 1.0)
+            refs.append(oracle.PllState(1.0, 0.0, 0.0, 0.0, toff, 1.0))
+        d_st = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).cuda()
+        rng = np.random.default_rng(3)
+        t = np.arange(n) / 240000.0
+        x = np.stack([(0.05 * np.cos(2 * np.pi * freq * t + 0.1 * c) + 0.02 * rng.standard_normal(n))
+                      .astype(np.float32) for c in range(nch)])
+        d_out = torch.zeros(nch, n + 1, device="cuda")
+        pkg.fmpll(d_out, torch.from_numpy(x).cuda(), freq, 240000.0, d_st, nco, 0.0, bw)
+        out = d_out.cpu().numpy()
+        for c in range(nch):
+            o = np.zeros(n + 1, np.float32)
+            o[-1] = 1.0
+            oracle.fmpll(x[c], freq, 240000.0, o, refs[c], nco, 0.0, bw)
+            assert np.array_equal(_u32(out[c]), _u32(o)), f"toff {toff:g} ch {c}"

@@ -109,3 +109,26 @@ def test_rds_group_encoder_syndromes(synth):
     offs = [0x0FC, 0x198, 0x168, 0x1B4]
     for blk, off in zip(blocks, offs):
         assert syndrome(blk) == off
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_oracle_modes_123_golden(oracle, synth, mode):
+    """golden_modes123.json (the unmodified reference in modes 1-3, project.cpp:76-103): the oracle's
+    1.44 / 1.152 MS/s front ends and 147/800, 147/1280 resamplers, every output of 7 blocks."""
+    fix = json.loads((GOLD / "golden_modes123.json").read_text())
+    m = fix["modes"][str(mode)]
+    src = synth.FMMultiplexSource(fix["channel"])
+    iq = np.stack([src.next_block(m["block_iq"]) for _ in range(fix["nblocks"])])
+    assert sha(iq) == m["input_sha256"]
+    ch = oracle.Channel(mode, True)
+    for b, want in enumerate(m["blocks"]):
+        fm = ch.frontend(iq[b])
+        assert sha(fm) == want["fm_demod_sha256"], f"mode {mode} fm_demod block {b}"
+        assert sha(ch.mono(fm)) == want["mono_sha256"], f"mode {mode} mono block {b}"
+        assert sha(ch.stereo(fm)) == want["stereo_sha256"], f"mode {mode} stereo block {b}"
+        r = ch.rds(fm)
+        assert sha(r["rds_clean"]) == want["rds_clean_sha256"], f"mode {mode} rds_clean block {b}"
+        if "bits" in want:
+            assert r["offset"] == want["offset"] and _bitstr(r["bits"]) == want["bits"], f"mode {mode} bits {b}"
+        else:
+            assert r["bits"] is None

@@ -57,10 +57,23 @@ int main(int argc, char** argv) {
         if (c != gc) hb64++;
         if ((float)c != (float)gc) hb32++;
     }
-    std::printf("{\"n\": %ld, \"cos\": {\"f64_mismatch\": %ld, \"f32_mismatch\": %ld}, "
+    // large arguments (|t| >= 2^30, Payne-Hanek): PLL-like 2^30..2^36 and the whole f32 range
+    long nl = 0, lb64 = 0, lb32 = 0;
+    for (long i = 0; i < N / 4; i++) {
+        const double ex = (i & 1) ? 30.0 + 6.0 * U(rng) : 30.0 + 98.0 * U(rng);
+        const float t = (float)(std::exp2(ex) * (U(rng) < 0.5 ? -1 : 1));
+        double s, c;
+        pllm::dd_sincos_f32(t, &s, &c);
+        const double gc = std::cos((double)t), gs = std::sin((double)t);
+        nl++;
+        lb64 += (c != gc) + (s != gs);
+        lb32 += ((float)c != (float)gc) + ((float)s != (float)gs);
+    }
+    std::printf("{\"large\": {\"n\": %ld, \"f64_mismatch\": %ld, \"f32_mismatch\": %ld}, ", nl, lb64, lb32);
+    std::printf("\"n\": %ld, \"cos\": {\"f64_mismatch\": %ld, \"f32_mismatch\": %ld}, "
                 "\"sin\": {\"f64_mismatch\": %ld, \"f32_mismatch\": %ld}, "
                 "\"atan2\": {\"f64_mismatch\": %ld, \"f32_mismatch\": %ld}, "
                 "\"cos_near_f32_midpoint\": {\"n\": %ld, \"f64_mismatch\": %ld, \"f32_mismatch\": %ld}}\n",
                 N, bad64[0], bad32[0], bad64[1], bad32[1], bad64[2], bad32[2], nh, hb64, hb32);
-    return (bad32[0] | bad32[1] | bad32[2] | hb32) ? 1 : 0;
+    return (bad32[0] | bad32[1] | bad32[2] | hb32 | lb32) ? 1 : 0;
 }
