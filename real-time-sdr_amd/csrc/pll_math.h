@@ -305,6 +305,73 @@ PLLM_HD SinCosR sincos_r(float t) {
     return o;
 }
 
+// ------------------------------------------------------------------------------------------
+// v3 step pieces (k_pll): fewer instructions per step, same values.
+//  * sincos_rn: the reduction rounds -t (2/pi) against MAGIC + 1, so the low word of the rounded
+//    value is nq1 = 1 - q (mod 2^32) -- exactly what base_angle needs -- and kdn = -kd folds its
+//    sign into the two reduction fmas. PLL_POLY = 1 evaluates both kernels by Horner (2
+//    multiplies fewer than Estrin's z^2, z^4 powers, a longer dependent chain), 0 by Estrin.
+//  * base_angle_n(nlo, nq1, b, mr) = base_angle(nlo, 1 - nq1, b, mr): one 3-input add.
+// ------------------------------------------------------------------------------------------
+#ifndef PLL_POLY
+#define PLL_POLY 1
+#endif
+constexpr double MAGIC1 = 6755399441055745.0;   // 1.5 * 2^52 + 1
+
+struct SinCosRN {
+    double cr, sr;   // cos r, sin r (relative error < 2^-50)
+    double r;        // t - q pi/2 in [-pi/4, pi/4]
+    uint32_t nq1;    // 1 - q (mod 2^32)
+    uint32_t b;      // [r < 0]
+    uint32_t tie;    // min(tie_key64(cr), tie_key64(sr)); the roundings are safe iff tie > TIE_MIN
+};
+
+PLLM_HD void sincos_kernels(double r, double& cr, double& sr) {
+    const double z = r * r;
+#if PLL_POLY
+    double sp = fma_(z, S6, S5);
+    sp = fma_(z, sp, S4);
+    sp = fma_(z, sp, S3);
+    sp = fma_(z, sp, S2);
+    sp = fma_(z, sp, S1);
+    double cp = fma_(z, C5, C4);
+    cp = fma_(z, cp, C3);
+    cp = fma_(z, cp, C2);
+    cp = fma_(z, cp, C1);
+    cp = fma_(z, cp, -0.5);
+    sr = fma_(r * z, sp, r);
+    cr = fma_(z, cp, 1.0);
+#else
+    const double z2 = z * z;
+    const double z4 = z2 * z2;
+    const double sp = fma_(z4, fma_(z, S6, S5), fma_(z2, fma_(z, S4, S3), fma_(z, S2, S1)));
+    const double cp = fma_(z4, C5, fma_(z2, fma_(z, C4, C3), fma_(z, C2, C1)));
+    sr = fma_(r * z, sp, r);
+    cr = fma_(z2, cp, fma_(z, -0.5, 1.0));
+#endif
+}
+
+// valid for |t| < T_MAX (the caller checks the range)
+PLLM_HD SinCosRN sincos_rn(float t) {
+    const double x = (double)t;
+    const double kdp = fma_(x, -TWO_OVER_PI, MAGIC1);   // MAGIC1 + rint(-x 2/pi)
+    const double kdn = kdp - MAGIC1;                      // -kd
+    const double r = fma_(kdn, PIO2_LO, fma_(kdn, PIO2_HI, x));
+    SinCosRN o;
+    sincos_kernels(r, o.cr, o.sr);
+    o.r = r;
+    o.nq1 = (uint32_t)__builtin_bit_cast(uint64_t, kdp);
+    o.b = (uint32_t)(__builtin_bit_cast(uint64_t, r) >> 63);
+    const uint32_t tc = tie_key64(o.cr), ts = tie_key64(o.sr);
+    o.tie = tc < ts ? tc : ts;
+    return o;
+}
+
+PLLM_HD double base_angle_n(uint32_t nlo, uint32_t nq1, uint32_t b, double mr) {
+    const int m = (int)((nlo + nq1 + b) & 3u) - (int)(b + 1u);
+    return fma_((double)m, PIO2, mr);
+}
+
 // (a, b) <- i^q (a + i b): q mod 4 = 1 -> (-b, a), 2 -> (-a, -b), 3 -> (b, -a)
 template <typename T>
 PLLM_HD void rot_q(uint32_t q, T& a, T& b) {

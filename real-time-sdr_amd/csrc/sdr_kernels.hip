@@ -1115,7 +1115,7 @@ struct PllRegs {
     float fbI, fbQ, integ, ph;   // fbI, fbQ in the reduced frame: RN(cos r), RN(sin r) (pll_math.h)
     double toff;
     double c, s, mr;             // f64 cos r, sin r and -r of the previous step's t = q pi/2 + r
-    uint32_t q, b;               // its quadrant q and [r < 0]
+    uint32_t nq1, b;             // 1 - q (mod 2^32) for its quadrant q, and [r < 0]
 };
 
 // The carried rotation is rebuilt from the state's previous trigArg t = (float)(w*toff + phaseEst)
@@ -1130,9 +1130,9 @@ __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
     r.ph = st.phaseEst;
     r.toff = st.trigOffset;
     const float t_prev = (float)(w * r.toff + (double)r.ph);
-    const pllm::SinCosR sc = pllm::sincos_r(t_prev);
+    const pllm::SinCosRN sc = pllm::sincos_rn(t_prev);
     float fI = (float)sc.cr, fQ = (float)sc.sr;
-    pllm::rot_q(sc.q, fI, fQ);
+    pllm::rot_q(1u - sc.nq1, fI, fQ);
     const bool consistent = (__builtin_fabs((double)t_prev) < pllm::T_MAX) && sc.tie > pllm::TIE_MIN &&
                             fI == st.feedbackI && fQ == st.feedbackQ;
     if (consistent) {
@@ -1140,8 +1140,8 @@ __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
         r.fbQ = (float)sc.sr;
         r.c = sc.cr;
         r.s = sc.sr;
-        r.mr = sc.mr;
-        r.q = sc.q;
+        r.mr = -sc.r;
+        r.nq1 = sc.nq1;
         r.b = sc.b;
     } else {
         r.fbI = st.feedbackI;
@@ -1149,7 +1149,7 @@ __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
         r.c = 1.0;
         r.s = 0.0;
         r.mr = __builtin_nan("");
-        r.q = 0u;
+        r.nq1 = 1u;
         r.b = 0u;
     }
     return r;
@@ -1196,6 +1196,15 @@ __device__ __noinline__ void pll_sincos_ref(float t, double* s, double* c) {
         sincos((double)t, s, c);
 }
 
+// split accumulator of the phase detector's rounding test, per step: acc | (lo ^ hi) as ONE
+// v_bitop3_b32 (truth table 0xF6 = s0 | (s1 ^ s2)). Written out because the compiler otherwise
+// keeps all 16 (lo, hi) pairs of a chunk alive and compares them at its end.
+__device__ __forceinline__ uint32_t or_xor(uint32_t acc, uint32_t lo, uint32_t hi) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xf6" : "=v"(d) : "v"(acc), "v"(lo), "v"(hi));
+    return d;
+}
+
 // One step of pll.cpp:36-50. CHECKED: every result the fast path cannot prove is recomputed
 // with the f64 libm exactly as the reference (used for chunk redo and short tails).
 template <bool CHECKED, bool TAB>
@@ -1206,13 +1215,21 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
     const f2v fb = {r.fbI, -r.fbQ};
     const f2v ee = x * fb;
     const float eI0 = ee.x, eQ0 = ee.y;
-    const double base = pllm::base_angle(pllm::lo_word(rx), r.q, r.b, r.mr);
-    const pllm::Phase2 p = pllm::phase_detect_r(eI0, eQ0, r.c, r.s, rx, base);
-    float e = p.ef;
-    if (CHECKED && !((__builtin_fabs(p.e) < pllm::PI - 0x1p-30) && p.split == 0u)) {
-        float a = eI0, b = -eQ0;                              // eI - i eQ = i^q (eI0 - i eQ0)
-        pllm::rot_q(r.q, a, b);
-        e = pll_atan2_ref(-b, a);                             // pll.cpp:39
+    // pll.cpp:39: atan2(eQ, eI) = base + Y/X (pll_math.h phase_detect2), rounding proven below
+    const double base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
+    const double Y = pllm::fma_((double)eI0, r.s, (double)eQ0 * r.c);
+    const double ed = pllm::fma_(Y, rx, base);
+    const float lo = (float)(ed - pllm::EPS_ABS_E2), hi = (float)(ed + pllm::EPS_ABS_E2);
+    float e = hi;                                             // = RN32(ed) whenever lo == hi
+    if (CHECKED) {
+        if (!((__builtin_fabs(ed) < pllm::PI - 0x1p-30) && lo == hi)) {
+            float a = eI0, b = -eQ0;                          // eI - i eQ = i^q (eI0 - i eQ0)
+            pllm::rot_q(1u - r.nq1, a, b);
+            e = pll_atan2_ref(-b, a);                         // pll.cpp:39
+        }
+    } else {
+        pf.emax = fmax(pf.emax, __builtin_fabs(ed));
+        pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
     }
     r.integ = r.integ + Ki * e;                               // pll.cpp:41
     r.ph = r.ph + Kp * e + r.integ;                           // pll.cpp:42
@@ -1223,11 +1240,11 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
         r.toff += 1.0;                                        // pll.cpp:46
         t = (float)(w * r.toff + (double)r.ph);               // pll.cpp:47
     }
-    const pllm::SinCosR sc = pllm::sincos_r(t);
+    const pllm::SinCosRN sc = pllm::sincos_rn(t);
     r.c = sc.cr;
     r.s = sc.sr;
-    r.mr = sc.mr;
-    r.q = sc.q;
+    r.mr = -sc.r;
+    r.nq1 = sc.nq1;
     r.b = sc.b;
     r.fbI = (float)sc.cr;                                     // pll.cpp:49-50, reduced frame
     r.fbQ = (float)sc.sr;
@@ -1236,7 +1253,7 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
         if (!(in_range && sc.tie > pllm::TIE_MIN)) {
             double sv, cv;
             pll_sincos_ref(t, &sv, &cv);
-            pllm::rot_q(0u - r.q, cv, sv);                    // into the reduced frame, exactly
+            pllm::rot_q(r.nq1 - 1u, cv, sv);                  // into the reduced frame, exactly
             r.fbI = (float)cv;
             r.fbQ = (float)sv;
             r.c = cv;
@@ -1244,8 +1261,6 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
             if (!in_range) r.mr = __builtin_nan("");
         }
     } else {
-        pf.emax = fmax(pf.emax, __builtin_fabs(p.e));
-        pf.split |= p.split;
         pf.tie = min(pf.tie, sc.tie);
         if (!TAB) pf.tmax = fmaxf(pf.tmax, __builtin_fabsf(t));
     }
@@ -1364,7 +1379,7 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
     }
     if (TAB) r.toff = s0.trigOffset + (double)n;               // pll.cpp:46, n times (exact)
     // every field but lastCarrier (k_nco_out's); the feedback back in the frame of t
-    pllm::rot_q(r.q, r.fbI, r.fbQ);
+    pllm::rot_q(1u - r.nq1, r.fbI, r.fbQ);
     st[ch].feedbackI = r.fbI;
     st[ch].feedbackQ = r.fbQ;
     st[ch].integrator = r.integ;
@@ -1998,6 +2013,69 @@ PllJob rds_job(sdr_ctx* c) {      // rds.cpp:119: fmpll(gen_pilot, 114e3, if_Fs,
 
 }  // namespace
 
+namespace {
+// Scratch of the context-free PLL primitive (input reciprocals [nch][ts] f64 + phases [nch][ts]
+// f32): one buffer per (device, stream), reused in that stream's order and grown on demand, so
+// sdr_fmpll enqueues without synchronising. SDR_FMPLL_SCRATCH selects the older variants for the
+// diagnosis in DESIGN.md (tools/diag_fmpll_scratch.py): "sync" (hipMalloc, synchronise, hipFree),
+// "async" (two hipMallocAsync / hipFreeAsync pairs on the default pool).
+struct StreamScratch {
+    hipStream_t s;
+    int dev;
+    void* p;
+    size_t bytes;
+};
+std::mutex g_scratch_mu;
+std::vector<StreamScratch> g_scratch;
+
+int stream_scratch(hipStream_t s, size_t bytes, void** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto& e : g_scratch) {
+        if (e.s != s || e.dev != dev) continue;
+        if (e.bytes < bytes) {   // grow: work already queued on s may still read the old buffer
+            HIP_TRY(hipStreamSynchronize(s));
+            HIP_TRY(hipFree(e.p));
+            e.p = nullptr;
+            HIP_TRY(hipMalloc(&e.p, bytes));
+            e.bytes = bytes;
+        }
+        *out = e.p;
+        return SDR_OK;
+    }
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, bytes));
+    g_scratch.push_back({s, dev, p, bytes});
+    *out = p;
+    return SDR_OK;
+}
+
+// forget (and free) the scratch of a stream about to be destroyed
+int release_stream_scratch(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (size_t i = 0; i < g_scratch.size(); i++) {
+        if (g_scratch[i].s != s) continue;
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipFree(g_scratch[i].p));
+        g_scratch.erase(g_scratch.begin() + (long)i);
+        return SDR_OK;
+    }
+    return SDR_OK;
+}
+
+int fmpll_scratch_mode() {
+    static const int v = [] {
+        const char* e = std::getenv("SDR_FMPLL_SCRATCH");
+        if (e && std::strcmp(e, "sync") == 0) return 1;
+        if (e && std::strcmp(e, "async") == 0) return 2;
+        return 0;
+    }();
+    return v;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* sdr_last_error(void) { return g_err.c_str(); }
@@ -2005,6 +2083,12 @@ int sdr_version(void) { return 1; }
 
 int sdr_stream_create_cu_range(void** stream, int device, int first_cu, int n_cu, int exclude) {
     if (!stream) return fail(SDR_E_INVALID, "sdr_stream_create_cu_range: stream is NULL");
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    struct Restore {   // the caller's current device is left as it was
+        int d;
+        ~Restore() { (void)hipSetDevice(d); }
+    } restore{cur};
     HIP_TRY(hipSetDevice(device));
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -2025,6 +2109,8 @@ int sdr_stream_create_cu_range(void** stream, int device, int first_cu, int n_cu
 
 int sdr_stream_destroy(void* stream) {
     if (!stream) return fail(SDR_E_INVALID, "sdr_stream_destroy: stream is NULL");
+    const int rc = release_stream_scratch((hipStream_t)stream);
+    if (rc != SDR_OK) return rc;
     HIP_TRY(hipStreamDestroy((hipStream_t)stream));
     return SDR_OK;
 }
@@ -2638,18 +2724,35 @@ int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, 
               sdr_pll_state* state, float ncoScale, float phaseAdjust, float normBandwidth, void* stream) {
     if (!out || !in || !state || nch <= 0 || n < 0) return fail(SDR_E_INVALID, "fmpll: bad arguments");
     const size_t ts = round_up((size_t)std::max(n, 1), 4);
-    // one scratch allocation: the input reciprocals [nch][ts] f64, then the phases [nch][ts] f32.
-    // Plain hipMalloc/hipFree (hipFree waits for the kernels): with two stream-ordered
-    // hipMallocAsync/hipFreeAsync pairs per call the drop-in harness saw non-deterministic PLL
-    // outputs on ROCm 7.2 (tools/diag_dropin_pll.py), so this primitive stays synchronous.
+    const size_t rx_bytes = ts * nch * sizeof(double), t_bytes = ts * nch * sizeof(float);
+    const int mode = fmpll_scratch_mode();
+    hipStream_t s = S(stream);
+    if (mode == 2) {
+        void *rxp = nullptr, *tp = nullptr;
+        HIP_TRY(hipMallocAsync(&rxp, rx_bytes, s));
+        HIP_TRY(hipMallocAsync(&tp, t_bytes, s));
+        const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, static_cast<float*>(tp), ts,
+                                 static_cast<double*>(rxp), out, out_stride, state, ncoScale, phaseAdjust,
+                                 normBandwidth, s);
+        HIP_TRY(hipFreeAsync(rxp, s));
+        HIP_TRY(hipFreeAsync(tp, s));
+        return r;
+    }
     void* scratch = nullptr;
-    HIP_TRY(hipMalloc(&scratch, ts * nch * (sizeof(double) + sizeof(float))));
+    if (mode == 1) {
+        HIP_TRY(hipMalloc(&scratch, rx_bytes + t_bytes));
+    } else {
+        const int rc = stream_scratch(s, rx_bytes + t_bytes, &scratch);
+        if (rc != SDR_OK) return rc;
+    }
     double* rxbuf = static_cast<double*>(scratch);
     float* tbuf = reinterpret_cast<float*>(rxbuf + ts * nch);
     const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, tbuf, ts, rxbuf, out, out_stride, state, ncoScale,
-                             phaseAdjust, normBandwidth, S(stream));
-    HIP_TRY(hipStreamSynchronize(S(stream)));
-    HIP_TRY(hipFree(scratch));
+                             phaseAdjust, normBandwidth, s);
+    if (mode == 1) {
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipFree(scratch));
+    }
     return r;
 }
 

@@ -228,7 +228,8 @@ def test_fmpll_long_stream_shared_offset(pkg, oracle, torch_cuda):
     torch = torch_cuda
     n, freq, nco, bw = 7350, 114e3, 0.5, 0.001
     w = 2 * np.pi * np.float32(freq / 240000.0)
-    for toff in (float(int(0x1.6p29 / w) - n - 2), float(int(0x1.6p29 / w) + 5)):
+    bound = 1.375 * 2.0 ** 29   # PLL_TAB_WT_MAX
+    for toff in (float(int(bound / w) - n - 2), float(int(bound / w) + 5)):
         nch = 64
         d_st = pkg.pll_state_tensor(nch)
         arr = (pkg.PllState * nch)()

@@ -41,7 +41,7 @@ int main(int argc, char** argv) {
     }
     std::printf("sincos2: ok %ld fallback %ld (%.2e) mismatches %ld\n", sc_ok, sc_bad, (double)sc_bad / N, sc_mis);
 
-    // 1b) the reduced-frame sincos_r (k_pll) on the same argument mix: accepted roundings, rotated
+    // 1b) the reduced-frame sincos_rn (k_pll) on the same argument mix: accepted roundings, rotated
     // by i^q, must equal RN_f32(glibc cos t), RN_f32(glibc sin t)
     {
         long ok = 0, bad = 0, mis = 0;
@@ -55,17 +55,17 @@ int main(int argc, char** argv) {
                 t = (float)(std::exp2(-30.0 + 60.0 * U(rng2)) * ((i & 1) ? 1 : -1));
             }
             if (!(std::fabs(t) < pllm::T_MAX)) continue;
-            const pllm::SinCosR r = pllm::sincos_r(t);
+            const pllm::SinCosRN r = pllm::sincos_rn(t);
             if (!(r.tie > pllm::TIE_MIN)) { bad++; continue; }
             ok++;
             float c = (float)r.cr, sn = (float)r.sr;
-            pllm::rot_q(r.q, c, sn);
+            pllm::rot_q(1u - r.nq1, c, sn);
             if (c != (float)std::cos((double)t) || sn != (float)std::sin((double)t)) {
-                if (mis < 10) std::printf("sincos_r MISMATCH t=%.9g\n", t);
+                if (mis < 10) std::printf("sincos_rn MISMATCH t=%.9g\n", t);
                 mis++;
             }
         }
-        std::printf("sincos_r: ok %ld fallback %ld (%.2e) mismatches %ld\n", ok, bad, (double)bad / N, mis);
+        std::printf("sincos_rn: ok %ld fallback %ld (%.2e) mismatches %ld\n", ok, bad, (double)bad / N, mis);
         sc_mis += mis;
     }
 
@@ -177,15 +177,15 @@ int main(int argc, char** argv) {
         float rfbI = (float)std::cos((double)t0), rfbQ = (float)std::sin((double)t0), rinteg = 0, rph = 0;
         // kernel state: pll_load
         float integ = 0, ph = 0;
-        pllm::SinCosR sc = pllm::sincos_r(t0);
+        pllm::SinCosRN sc = pllm::sincos_rn(t0);
         float fI0 = (float)sc.cr, fQ0 = (float)sc.sr;
         {
             float a = fI0, b = fQ0;
-            pllm::rot_q(sc.q, a, b);
+            pllm::rot_q(1u - sc.nq1, a, b);
             if (a != rfbI || b != rfbQ) std::printf("load: inconsistent state\n");
         }
-        double cr = sc.cr, sr = sc.sr, mr = sc.mr;
-        uint32_t q = sc.q, bsg = sc.b;
+        double cr = sc.cr, sr = sc.sr, mr = -sc.r;
+        uint32_t nq1 = sc.nq1, bsg = sc.b;
         const long n = N / 8;
         for (long i = 0; i < n; i++) {
             const float xin = (float)(0.1 * std::cos(2 * M_PI * (freq + 3.0 * sig) / Fs * i + sig) +
@@ -203,12 +203,12 @@ int main(int argc, char** argv) {
             {
                 const float eI0 = xin * fI0, eQ0 = xin * (-fQ0);
                 const double rx = pllm::pll_rx(xin);
-                const double base = pllm::base_angle(pllm::lo_word(rx), q, bsg, mr);
+                const double base = pllm::base_angle_n(pllm::lo_word(rx), nq1, bsg, mr);
                 const pllm::Phase2 p = pllm::phase_detect_r(eI0, eQ0, cr, sr, rx, base);
                 float e = p.ef;
                 if (!(std::fabs(p.e) < pllm::PI - 0x1p-30 && p.split == 0u)) {
                     float a = eI0, b = -eQ0;
-                    pllm::rot_q(q, a, b);
+                    pllm::rot_q(1u - nq1, a, b);
                     e = (float)std::atan2((double)(-b), (double)a);
                     rfb_e++;
                 }
@@ -216,12 +216,12 @@ int main(int argc, char** argv) {
                 ph = ph + Kp * e + integ;
                 toff += 1.0;
                 const float t = (float)(w * toff + (double)ph);
-                sc = pllm::sincos_r(t);
-                cr = sc.cr; sr = sc.sr; mr = sc.mr; q = sc.q; bsg = sc.b;
+                sc = pllm::sincos_rn(t);
+                cr = sc.cr; sr = sc.sr; mr = -sc.r; nq1 = sc.nq1; bsg = sc.b;
                 fI0 = (float)cr; fQ0 = (float)sr;
                 if (!(sc.tie > pllm::TIE_MIN)) {
                     double cv = std::cos((double)t), sv = std::sin((double)t);
-                    pllm::rot_q(0u - q, cv, sv);
+                    pllm::rot_q(nq1 - 1u, cv, sv);
                     cr = cv; sr = sv;
                     fI0 = (float)cr; fQ0 = (float)sr;
                     rfb_sc++;
@@ -229,7 +229,7 @@ int main(int argc, char** argv) {
             }
             rsteps++;
             float fbI = fI0, fbQ = fQ0;
-            pllm::rot_q(q, fbI, fbQ);
+            pllm::rot_q(1u - nq1, fbI, fbQ);
             if (fbI != rfbI || fbQ != rfbQ || ph != rph || integ != rinteg) {
                 if (rdiff < 5) std::printf("reduced-frame PLL diverged sig %d step %ld\n", sig, i);
                 rdiff++;
