@@ -2069,6 +2069,8 @@ int fmpll_scratch_mode() {
         const char* e = std::getenv("SDR_FMPLL_SCRATCH");
         if (e && std::strcmp(e, "sync") == 0) return 1;
         if (e && std::strcmp(e, "async") == 0) return 2;
+        if (e && std::strcmp(e, "async_leak") == 0) return 3;      // hipMallocAsync, never freed
+        if (e && std::strcmp(e, "async_syncalloc") == 0) return 4; // hipMallocAsync + synchronise, then launch
         return 0;
     }();
     return v;
@@ -2727,15 +2729,18 @@ int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, 
     const size_t rx_bytes = ts * nch * sizeof(double), t_bytes = ts * nch * sizeof(float);
     const int mode = fmpll_scratch_mode();
     hipStream_t s = S(stream);
-    if (mode == 2) {
+    if (mode >= 2) {
         void *rxp = nullptr, *tp = nullptr;
         HIP_TRY(hipMallocAsync(&rxp, rx_bytes, s));
         HIP_TRY(hipMallocAsync(&tp, t_bytes, s));
+        if (mode == 4) HIP_TRY(hipStreamSynchronize(s));
         const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, static_cast<float*>(tp), ts,
                                  static_cast<double*>(rxp), out, out_stride, state, ncoScale, phaseAdjust,
                                  normBandwidth, s);
-        HIP_TRY(hipFreeAsync(rxp, s));
-        HIP_TRY(hipFreeAsync(tp, s));
+        if (mode != 3) {
+            HIP_TRY(hipFreeAsync(rxp, s));
+            HIP_TRY(hipFreeAsync(tp, s));
+        }
         return r;
     }
     void* scratch = nullptr;

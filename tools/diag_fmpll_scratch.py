@@ -30,7 +30,7 @@ with tempfile.TemporaryDirectory() as d:
     subprocess.run([str(ROOT / "oracle/_ref/ref_harness"), str(inp), str(nb), "0", "1", f"{d}/cpu_"], check=True,
                    timeout=300)
     ref = {o: pathlib.Path(f"{d}/cpu_{o}").read_bytes() for o in OUTS}
-    for mode in ("stream", "sync", "async"):
+    for mode in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("stream", "sync", "async")):
         runs = []
         for r in range(reps):
             env = dict(os.environ, SDR_FMPLL_SCRATCH=mode)
