@@ -173,6 +173,10 @@ class GpuStepper:
                 cu_spec = ""
         self.cu_spec = cu_spec
         self.s_fe, self.s_pll, self.s_post = s_fe, s_pll, s_post
+        # SDR_BENCH_PLL=persistent (default): one PLL dispatch per phase (warm-up, timed) that waits
+        # for each block's device flag (sdr_plls_launch/_signal/_wait); "dispatch": one sdr_plls
+        # dispatch per block, ordered by events
+        self.persist = os.environ.get("SDR_BENCH_PLL", "persistent") == "persistent"
         self.s_gather = torch.cuda.Stream(dev)       # torch pool streams are non-blocking
         self.mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
         self.lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]
@@ -198,6 +202,11 @@ class GpuStepper:
         return {"lr": ((self.nch, 2 * self.info.n_audio), self.torch.int16),
                 "bits": ((self.nch, self.pkg.SDR_MAX_BITS), self.torch.uint8)}
 
+    def begin_phase(self, nblocks: int) -> None:
+        """Before the warm-up and before the timed blocks: the persistent PLL dispatch of the phase."""
+        if self.persist:
+            self.pipe.plls_launch(nblocks, stream=self.s_pll)
+
     def step(self, b: int, gather=None) -> None:
         torch, pipe = self.torch, self.pipe
         s_fe, s_pll, s_post = self.s_fe, self.s_pll, self.s_post
@@ -213,12 +222,16 @@ class GpuStepper:
             torch.index_select(self.mono, 0, self.vsel, out=self.cap_mono[b])
         pipe.stereo_pre(stream=s_fe)                          # stereo.cpp:74, :80
         pipe.rds_pre(stream=s_fe)                             # rds.cpp:105-116
-        self.pre_done[b].record(s_fe)
-        s_pll.wait_event(self.pre_done[b])
-        self.pll_start[b].record(s_pll)
-        pipe.plls(stream=s_pll)                               # stereo.cpp:77 + rds.cpp:119
-        self.pll_done[b].record(s_pll)
-        s_post.wait_event(self.pll_done[b])
+        if self.persist:                                      # stereo.cpp:77 + rds.cpp:119
+            pipe.plls_signal(stream=s_fe)
+            pipe.plls_wait(stream=s_post)
+        else:
+            self.pre_done[b].record(s_fe)
+            s_pll.wait_event(self.pre_done[b])
+            self.pll_start[b].record(s_pll)
+            pipe.plls(stream=s_pll)
+            self.pll_done[b].record(s_pll)
+            s_post.wait_event(self.pll_done[b])
         if gather is not None and b >= 2:
             s_post.wait_event(self.gather_done[b - 2])        # lr/bits slot of block b-2 gathered
         lr, bits = self.lr[b % 2], self.bits[b % 2]
@@ -247,7 +260,10 @@ class GpuStepper:
         rng = range(warmup, self.nblocks)
         fe_avg_s = float(np.mean([self.fe_start[b].elapsed_time(self.fe_end[b]) for b in rng])) / 1e3
         fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
-        pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
+        if self.persist:   # device-clock time of each block inside the timed phase's dispatch
+            pll_ms = float(np.mean(self.pipe.plls_report(stream=self.s_pll)))
+        else:
+            pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
         achieved = fe_bytes / fe_avg_s / 1e9
         kname = ("k_frontend_mfma" if self.fast else "k_frontend2") + " (u8 I/Q -> 101-tap FIR /10 on I,Q -> FM discriminator)"
         return {
@@ -255,8 +271,9 @@ class GpuStepper:
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": _pmc_traffic(nch, self.args.numerics),
                          "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4)},
-            "pll": {"kernel": "k_pll: stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial "
-                              "chains in one dispatch",
+            "pll": {"kernel": ("k_pll_multi: persistent, all blocks of the phase in one dispatch" if self.persist
+                               else "k_pll: one dispatch per block") +
+                              ", stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial chains",
                     "bound": "serial recurrence: block_if dependent steps per chain, one lane per chain "
                              "(per-wave VALU issue, DESIGN.md 4a)",
                     "avg_launch_ms": round(pll_ms, 4), "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
@@ -342,6 +359,8 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
         bg = BlockGather(torch, dist, world, st.outputs_spec(), gdev, dst=0)
     gather = bg.gather if bg is not None else None
     try:
+        if hasattr(st, "begin_phase") and args.warmup:
+            st.begin_phase(args.warmup)
         for b in range(args.warmup):
             st.step(b, gather)
         st.synchronize()
@@ -349,6 +368,8 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
             dist.barrier()
         st.synchronize()
         t0 = time.perf_counter()
+        if hasattr(st, "begin_phase"):
+            st.begin_phase(args.steps)
         for b in range(args.warmup, nblocks):
             st.step(b, gather)
         st.synchronize()

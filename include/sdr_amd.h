@@ -144,6 +144,18 @@ int sdr_rds_post(sdr_ctx *ctx, float *rds_clean, size_t rds_stride, void *stream
 /* stereo_pll + rds_pll of the current block in one dispatch (2 x nch independent recurrences);
  * needs both _pre parts done. */
 int sdr_plls(sdr_ctx *ctx, void *stream);
+/* Persistent PLLs: the stereo + RDS PLLs of many consecutive blocks in ONE dispatch (no launch
+ * gap between blocks). sdr_plls_launch(nblocks) on the PLL stream, before the sdr_frontend of the
+ * first of those blocks; then per block, after both _pre parts, sdr_plls_signal on the stream that
+ * ran them (instead of sdr_plls) and sdr_plls_wait on the stream of the _post parts. The kernel
+ * waits for each block's signal (a device flag written in stream order), runs both PLLs, and
+ * releases the waiting stream; a wait longer than 5 s ends the launch without computing and is
+ * reported by sdr_plls_report, which also returns each block's PLL time of the last launch (ms,
+ * from the device clock) and synchronises `stream`. Not with SDR_FLAG_PLL_LIBM. */
+int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
+int sdr_plls_signal(sdr_ctx *ctx, void *stream);
+int sdr_plls_wait(sdr_ctx *ctx, void *stream);
+int sdr_plls_report(sdr_ctx *ctx, double *block_ms, int max_blocks, int *nblocks, void *stream);
 /* rds symbol/bit recovery (rds.cpp:135-167): per channel, for blocks with block_count > 5 and
  * rds_on: offset = cdr(), symbols (0/1 bytes), bits (decoded 0/1 bytes). nbits[ch] = -1 on
  * blocks that do not decode. Any output pointer may be NULL. Strides in elements. */

@@ -87,6 +87,10 @@ def lib() -> C.CDLL:
         "sdr_rds_pre": ([vp, vp], i32),
         "sdr_rds_pll": ([vp, vp], i32),
         "sdr_plls": ([vp, vp], i32),
+        "sdr_plls_launch": ([vp, i32, vp], i32),
+        "sdr_plls_signal": ([vp, vp], i32),
+        "sdr_plls_wait": ([vp, vp], i32),
+        "sdr_plls_report": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32), vp], i32),
         "sdr_rds_post": ([vp, vp, sz, vp], i32),
         "sdr_ctx_buffer": ([vp, C.c_char_p, C.POINTER(vp), C.POINTER(sz), C.POINTER(i32)], i32),
     }
@@ -300,6 +304,23 @@ class Pipeline:
     def plls(self, stream=None):
         """stereo_pll + rds_pll in one dispatch."""
         check(lib().sdr_plls(self._h, _stream(stream)), "sdr_plls")
+
+    # persistent PLLs (include/sdr_amd.h): one dispatch for many blocks
+    def plls_launch(self, nblocks: int, stream=None):
+        check(lib().sdr_plls_launch(self._h, nblocks, _stream(stream)), "sdr_plls_launch")
+
+    def plls_signal(self, stream=None):
+        check(lib().sdr_plls_signal(self._h, _stream(stream)), "sdr_plls_signal")
+
+    def plls_wait(self, stream=None):
+        check(lib().sdr_plls_wait(self._h, _stream(stream)), "sdr_plls_wait")
+
+    def plls_report(self, max_blocks: int = 4096, stream=None) -> list:
+        """Per-block PLL time (ms) of the last persistent launch; raises if a wait timed out."""
+        arr = (C.c_double * max_blocks)()
+        n = C.c_int(0)
+        check(lib().sdr_plls_report(self._h, arr, max_blocks, C.byref(n), _stream(stream)), "sdr_plls_report")
+        return list(arr[:n.value])
 
     def rds_post(self, out=None, bits=True, stream=None):
         check(lib().sdr_rds_post(self._h, _ptr(out), _row_stride(out) if out is not None else 0, _stream(stream)),

@@ -1416,6 +1416,74 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
     else pll_run<VEC, false>(jb, n, ch, nullptr);
 }
 
+// ------------------------------------------------------------------------------------------
+// Persistent PLLs (sdr_plls_launch / _signal / _wait): one dispatch runs the PLLs of `nblocks`
+// consecutive blocks, so consecutive blocks are not separated by a dispatch (the ~19 us gap
+// between back-to-back k_pll launches). Before block j the waves wait, with an
+// agent-scope acquire, for the front-end stream's flag (written by hipStreamWriteValue32 after
+// the pre-PLL stage of that block); after it each wave adds 1 to a done counter with an
+// agent-scope release, which the post stream waits on (hipStreamWaitValue32). Blocks alternate
+// the context's two buffer parities. Every wait is bounded: after PLL_WAIT_TICKS of the 100 MHz
+// clock the launch records an error and completes its remaining blocks without computing, so no
+// wave and no waiting stream can hang.
+// ------------------------------------------------------------------------------------------
+struct PllJobs2 {
+    PllJobs p[2];
+};
+constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrealtime
+
+template <bool VEC>
+__global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
+                                                  int first_parity, const uint32_t* pre_flag, uint32_t pre_first,
+                                                  uint32_t* done_count, uint32_t* err,
+                                                  unsigned long long* t_start, unsigned long long* t_end) {
+    extern __shared__ double wtab[];
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = ch < nch;
+    __builtin_amdgcn_s_setprio(3);
+    bool dead = false;
+    for (int j = 0; j < nblocks; j++) {
+        const PllJob& jb = jobs.p[(first_parity + j) & 1].j[blockIdx.y];
+        if (!dead) {
+            const uint32_t want = pre_first + (uint32_t)j + 1u;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while ((int32_t)(__hip_atomic_load(pre_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+                __builtin_amdgcn_s_sleep(4);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
+                    dead = true;
+                    break;
+                }
+            }
+            if (dead && threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!dead) {
+            if (threadIdx.x == 0)
+                __hip_atomic_fetch_min(t_start + j, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double toff0 = active ? jb.st[ch].trigOffset : 0.0;
+            const double w = 2 * 3.14159265358979323846 * (jb.freq / jb.Fs);
+            const double toff_l0 = __shfl(toff0, 0);
+            const bool tab = tab_ok && __all(!active || toff0 == toff_l0) &&
+                             __builtin_fabs(w) * (__builtin_fabs(toff_l0) + (double)n + 1.0) < PLL_TAB_WT_MAX;
+            if (tab) {
+                for (int k = threadIdx.x; k < n; k += 64) wtab[k] = w * (toff_l0 + (double)(k + 1));   // pll.cpp:46-47
+                __syncthreads();
+            }
+            if (active) {
+                if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
+                else pll_run<VEC, false>(jb, n, ch, nullptr);
+            }
+            __syncthreads();   // every lane's table reads and state/phase stores issued before the release
+        }
+        if (threadIdx.x == 0) {
+            if (!dead)
+                __hip_atomic_fetch_max(t_end + j, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(done_count, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // pll_rx of a PLL input with no fused producer (the batched sdr_fmpll primitive)
 __global__ __launch_bounds__(BLK) void k_pll_rx(double* __restrict__ rx, size_t rx_stride, const float* __restrict__ x,
                                                 size_t x_stride, int n) {
@@ -1902,6 +1970,14 @@ struct sdr_ctx {
     long long block = -1;                               // index of the current block
     long long stereo_done = -1, rds_dsp_done = -1, rds_bits_done = -1, mono_done = -1;
     long long st_pre_done = -1, st_pll_done = -1, rds_pre_done = -1, rds_pll_done = -1;
+    // persistent PLLs (sdr_plls_launch / _signal / _wait): device words [pre_flag, done_count,
+    // err], per-block timestamps of the last launch, and the host's sequence bookkeeping
+    uint32_t* pers_words = nullptr;
+    unsigned long long *pers_t0 = nullptr, *pers_t1 = nullptr;
+    int pers_tcap = 0, pers_last_n = 0;
+    uint32_t pers_launched = 0, pers_signaled = 0, pers_waves = 0;
+    long long pers_block = -1;                          // block of the last signal
+    uint32_t pers_block_seq = 0;                        // its sequence number
     std::vector<void*> allocs;
 
     float* fm_cur() const { return fm + parity * fm_par; }
@@ -2523,6 +2599,104 @@ int sdr_plls(sdr_ctx* c, void* stream) {
     const int r = launch_plls(c->flags & SDR_FLAG_PLL_LIBM, jobs, 2, c->info.block_if, c->nch, S(stream), false);
     if (r) return r;
     c->st_pll_done = c->rds_pll_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
+    if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_launch: bad arguments");
+    if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_launch: not with SDR_FLAG_PLL_LIBM");
+    if (c->pers_signaled != c->pers_launched)
+        return fail(SDR_E_INVALID, "plls_launch: the previous launch still has %u blocks to signal",
+                    c->pers_launched - c->pers_signaled);
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = S(stream);
+    if (!c->pers_words) {
+        const int r = dalloc(c, &c->pers_words, 4);
+        if (r) return r;
+    }
+    if (c->pers_tcap < nblocks) {   // grow the timestamp arrays (the previous launch finished first)
+        HIP_TRY(hipStreamSynchronize(s));
+        int r = dalloc(c, &c->pers_t0, (size_t)nblocks);
+        if (!r) r = dalloc(c, &c->pers_t1, (size_t)nblocks);
+        if (r) return r;
+        c->pers_tcap = nblocks;
+    }
+    HIP_TRY(hipMemsetAsync(c->pers_t0, 0xFF, (size_t)nblocks * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(c->pers_t1, 0, (size_t)nblocks * sizeof(unsigned long long), s));
+    const int n = c->info.block_if, nch = c->nch;
+    PllJobs2 jobs{};
+    const int first_parity = c->parity ^ 1;   // the parity the next sdr_frontend switches to
+    for (int k = 0; k < 2; k++) {
+        const int saved = c->parity;
+        c->parity = first_parity ^ k;
+        jobs.p[k].j[0] = stereo_job(c);
+        jobs.p[k].j[1] = rds_job(c);
+        c->parity = saved;
+    }
+    bool vec = true;
+    for (int k = 0; k < 2; k++)
+        for (int q = 0; q < 2; q++) {
+            const PllJob& j = jobs.p[k].j[q];
+            vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
+                  (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
+                  (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0);
+        }
+    const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
+    const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
+    const dim3 g(cdiv(nch, 64), 2), b(64);
+    c->pers_waves = g.x * g.y;
+    uint32_t* w = c->pers_words;
+    if (vec)
+        hipLaunchKernelGGL(k_pll_multi<true>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
+                           first_parity, w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1);
+    else
+        hipLaunchKernelGGL(k_pll_multi<false>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
+                           first_parity, w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1);
+    LAUNCH_CHECK();
+    c->pers_launched += (uint32_t)nblocks;
+    c->pers_last_n = nblocks;
+    return SDR_OK;
+}
+
+int sdr_plls_signal(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->st_pre_done != c->block || c->rds_pre_done != c->block || c->st_pll_done == c->block ||
+        c->rds_pll_done == c->block)
+        return fail(SDR_E_INVALID, "plls_signal: run sdr_stereo_pre and sdr_rds_pre on a new block first");
+    if (c->pers_signaled == c->pers_launched)
+        return fail(SDR_E_INVALID, "plls_signal: no sdr_plls_launch covers this block");
+    HIP_TRY(hipStreamWriteValue32(S(stream), c->pers_words, c->pers_signaled + 1u, 0));
+    c->pers_block = c->block;
+    c->pers_block_seq = c->pers_signaled;
+    c->pers_signaled++;
+    c->st_pll_done = c->rds_pll_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_plls_wait(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->pers_block != c->block) return fail(SDR_E_INVALID, "plls_wait: sdr_plls_signal this block first");
+    const uint32_t want = c->pers_waves * (c->pers_block_seq + 1u);
+    HIP_TRY(hipStreamWaitValue32(S(stream), c->pers_words + 1, want, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    return SDR_OK;
+}
+
+int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, void* stream) {
+    if (!c || !c->pers_words) return fail(SDR_E_INVALID, "plls_report: no persistent launch");
+    hipStream_t s = S(stream);
+    const int n = std::min(c->pers_last_n, std::max(max_blocks, 0));
+    std::vector<unsigned long long> t0((size_t)std::max(n, 1)), t1((size_t)std::max(n, 1));
+    uint32_t words[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(words, c->pers_words, sizeof(words), hipMemcpyDeviceToHost, s));
+    if (n > 0) {
+        HIP_TRY(hipMemcpyAsync(t0.data(), c->pers_t0, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(t1.data(), c->pers_t1, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int j = 0; j < n && block_ms; j++)   // s_memrealtime: 100 MHz
+        block_ms[j] = (t1[j] >= t0[j]) ? (double)(t1[j] - t0[j]) * 1e-5 : -1.0;
+    if (nblocks) *nblocks = n;
+    if (words[2]) return fail(SDR_E_HIP, "plls_report: a persistent PLL wait timed out (outputs invalid)");
     return SDR_OK;
 }
 

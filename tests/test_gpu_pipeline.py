@@ -224,8 +224,8 @@ def test_fast_frontend_tolerance_and_rds_bits(pkg, synth, golden_long, oracle, t
                 assert _bitstr(out["bits"][b][j], int(out["nbits"][b][j])) == want["bits"], f"bits ch{c} block {b}"
 
 
-@pytest.mark.parametrize("fused_plls,cu_masked", [(False, False), (True, False), (True, True)],
-                         ids=["two_pll_streams", "sdr_plls", "sdr_plls_cu_masked"])
+@pytest.mark.parametrize("fused_plls,cu_masked", [(False, False), (True, False), (True, True), ("persistent", True)],
+                         ids=["two_pll_streams", "sdr_plls", "sdr_plls_cu_masked", "persistent_cu_masked"])
 def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_plls, cu_masked):
     """bench.py's schedule: the stereo/RDS bodies split at the PLL (sdr_*_pre/_pll/_post, or both
     PLLs in one sdr_plls dispatch) on separate streams with the PLLs of block b+1 overlapping block
@@ -256,7 +256,11 @@ def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_
     mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device="cuda")
     clean = torch.empty(nch, info.n_rds, dtype=torch.float32, device="cuda")
     got = {"mono": [], "stereo": [], "clean": [], "bits": [], "nbits": []}
+    if fused_plls == "persistent":   # two launches: the second covers the rest
+        pipe.plls_launch(5, stream=s_pst)
     for b in range(nb):
+        if fused_plls == "persistent" and b == 5:
+            pipe.plls_launch(nb - 5, stream=s_pst)
         if b >= 2:
             s_fe.wait_event(post[b - 2])
         pipe.frontend(d[b], stream=s_fe)
@@ -266,7 +270,10 @@ def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_
         pipe.stereo_pre(stream=s_fe)
         pipe.rds_pre(stream=s_fe)
         pre[b].record(s_fe)
-        if fused_plls:
+        if fused_plls == "persistent":   # no events: device flags written / waited in stream order
+            pipe.plls_signal(stream=s_fe)
+            pipe.plls_wait(stream=s_post)
+        elif fused_plls:
             s_pst.wait_event(pre[b])
             pipe.plls(stream=s_pst)
             pst[b].record(s_pst)
@@ -278,8 +285,9 @@ def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_
             s_prd.wait_event(pre[b])
             pipe.rds_pll(stream=s_prd)
             prd[b].record(s_prd)
-        s_post.wait_event(pst[b])
-        s_post.wait_event(prd[b])
+        if fused_plls != "persistent":
+            s_post.wait_event(pst[b])
+            s_post.wait_event(prd[b])
         pipe.stereo_post(lr[b % 2], stream=s_post)
         pipe.rds_post(clean, bits=True, stream=s_post)
         with torch.cuda.stream(s_post):
@@ -289,6 +297,9 @@ def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_
             got["nbits"].append(pipe.nbits.clone())
         post[b].record(s_post)
     torch.cuda.synchronize()
+    if fused_plls == "persistent":
+        ms = pipe.plls_report(stream=s_pst)
+        assert len(ms) == nb - 5 and all(0 < m < 100 for m in ms), ms
     for h in handles:
         assert pkg.lib().sdr_stream_destroy(C.c_void_p(h)) == 0
     for b in range(nb):
@@ -350,3 +361,30 @@ def test_fast_frontend_all_outputs_tolerance(pkg, synth, golden_long, oracle, to
                 bad.append(f"nbits ch{c} block {b}")
     print("fast front end worst (acquisition, locked):", worst)
     assert not bad, f"{len(bad)} out of bounds: {bad[:12]}"
+
+
+def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda):
+    """A persistent launch whose last block is never signalled ends by itself (bounded wait, 5 s),
+    releases its done counter and reports the error; blocks before it are computed normally."""
+    torch = torch_cuda
+    nch, nb = 8, 3
+    iqs = [channel_input(synth, 500 + c, nb) for c in range(nch)]
+    d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
+    ref = _run_pipeline(pkg, torch, iqs, nb - 1)
+    pipe = pkg.Pipeline(nch)
+    s_pll, s_post = torch.cuda.Stream(), torch.cuda.Stream()
+    pipe.plls_launch(nb, stream=s_pll)
+    lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
+    for b in range(nb - 1):
+        pipe.frontend(d[b])
+        pipe.stereo_pre()
+        pipe.rds_pre()
+        pipe.plls_signal()
+        pipe.plls_wait(stream=s_post)
+        pipe.stereo_post(lr, stream=s_post)
+        pipe.rds_post(None, bits=False, stream=s_post)
+        torch.cuda.synchronize()
+        assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
+    with pytest.raises(pkg.SdrError, match="timed out"):
+        pipe.plls_report(stream=s_pll)
+    pipe.close()
