@@ -1420,9 +1420,12 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
 // Persistent PLLs (sdr_plls_launch / _signal / _wait): one dispatch runs the PLLs of `nblocks`
 // consecutive blocks, so consecutive blocks are not separated by a dispatch (the ~19 us gap
 // between back-to-back k_pll launches). Before block j the waves wait, with an
-// agent-scope acquire, for the front-end stream's flag (written by hipStreamWriteValue32 after
-// the pre-PLL stage of that block); after it each wave adds 1 to a done counter with an
-// agent-scope release, which the post stream waits on (hipStreamWaitValue32). Blocks alternate
+// agent-scope acquire, for the front-end stream's flag (k_flag_store, dispatched after the
+// pre-PLL kernels of that block); after it each wave adds 1 to a done counter with an
+// agent-scope release, which the post stream waits on (k_flag_wait). hipStreamWriteValue32 is
+// not used for the flag: in a first version its write overtook the still-running pre-PLL kernel
+// (the first block of a launch, whose waves are already waiting, read inputs before they were
+// complete), while a kernel dispatch starts only after its predecessor has completed. Blocks alternate
 // the context's two buffer parities. Every wait is bounded: after PLL_WAIT_TICKS of the 100 MHz
 // clock the launch records an error and completes its remaining blocks without computing, so no
 // wave and no waiting stream can hang.
@@ -1480,6 +1483,26 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
                 __hip_atomic_fetch_max(t_end + j, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(done_count, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// The two ends of the persistent PLLs' hand-offs, as one-wave kernels so that HIP's in-order
+// kernel dispatch (each dispatch starts after the previous one in its stream has completed and
+// released its writes) orders them: k_flag_store publishes "block ready" after the pre-PLL
+// kernels of the front-end stream; k_flag_wait holds the post stream until the PLL waves have
+// released a block (bounded, like the PLL's own waits).
+__global__ void k_flag_store(uint32_t* flag, uint32_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void k_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int32_t)(__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+        __builtin_amdgcn_s_sleep(4);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
+            __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
         }
     }
 }
@@ -2665,7 +2688,8 @@ int sdr_plls_signal(sdr_ctx* c, void* stream) {
         return fail(SDR_E_INVALID, "plls_signal: run sdr_stereo_pre and sdr_rds_pre on a new block first");
     if (c->pers_signaled == c->pers_launched)
         return fail(SDR_E_INVALID, "plls_signal: no sdr_plls_launch covers this block");
-    HIP_TRY(hipStreamWriteValue32(S(stream), c->pers_words, c->pers_signaled + 1u, 0));
+    hipLaunchKernelGGL(k_flag_store, dim3(1), dim3(64), 0, S(stream), c->pers_words, c->pers_signaled + 1u);
+    LAUNCH_CHECK();
     c->pers_block = c->block;
     c->pers_block_seq = c->pers_signaled;
     c->pers_signaled++;
@@ -2677,7 +2701,8 @@ int sdr_plls_wait(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (c->pers_block != c->block) return fail(SDR_E_INVALID, "plls_wait: sdr_plls_signal this block first");
     const uint32_t want = c->pers_waves * (c->pers_block_seq + 1u);
-    HIP_TRY(hipStreamWaitValue32(S(stream), c->pers_words + 1, want, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    hipLaunchKernelGGL(k_flag_wait, dim3(1), dim3(64), 0, S(stream), c->pers_words + 1, want, c->pers_words + 2);
+    LAUNCH_CHECK();
     return SDR_OK;
 }
 

@@ -383,7 +383,7 @@ def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda):
         pipe.plls_wait(stream=s_post)
         pipe.stereo_post(lr, stream=s_post)
         pipe.rds_post(None, bits=False, stream=s_post)
-        torch.cuda.synchronize()
+        s_post.synchronize()   # not torch.cuda.synchronize(): the persistent PLL is still running
         assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
     with pytest.raises(pkg.SdrError, match="timed out"):
         pipe.plls_report(stream=s_pll)
