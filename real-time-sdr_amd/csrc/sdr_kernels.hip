@@ -1439,7 +1439,8 @@ template <bool VEC>
 __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
                                                   int first_parity, const uint32_t* pre_flag, uint32_t pre_first,
                                                   uint32_t* done_count, uint32_t* err,
-                                                  unsigned long long* t_start, unsigned long long* t_end) {
+                                                  unsigned long long* t_start, unsigned long long* t_end,
+                                                  int sys_acquire) {
     extern __shared__ double wtab[];
     const int ch = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = ch < nch;
@@ -1450,7 +1451,9 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
         if (!dead) {
             const uint32_t want = pre_first + (uint32_t)j + 1u;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while ((int32_t)(__hip_atomic_load(pre_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+            while ((int32_t)((sys_acquire ? __hip_atomic_load(pre_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : __hip_atomic_load(pre_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) -
+                             want) < 0) {
                 __builtin_amdgcn_s_sleep(4);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
                     dead = true;
@@ -2668,13 +2671,15 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
     const dim3 g(cdiv(nch, 64), 2), b(64);
     c->pers_waves = g.x * g.y;
+    const char* acq = std::getenv("SDR_PLL_ACQUIRE");   // diagnosis: system-scope acquire
+    const int sys_acq = (acq && std::strcmp(acq, "system") == 0) ? 1 : 0;
     uint32_t* w = c->pers_words;
     if (vec)
         hipLaunchKernelGGL(k_pll_multi<true>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
-                           first_parity, w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1);
+                           first_parity, w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1, sys_acq);
     else
         hipLaunchKernelGGL(k_pll_multi<false>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
-                           first_parity, w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1);
+                           first_parity, w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1, sys_acq);
     LAUNCH_CHECK();
     c->pers_launched += (uint32_t)nblocks;
     c->pers_last_n = nblocks;
