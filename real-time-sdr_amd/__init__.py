@@ -349,8 +349,10 @@ class Pipeline:
                                      _stream(stream)), "sdr_rds_bits")
         return out
 
-    def buffer(self, name: str):
-        """Current-block intermediate as a [nch][len] torch view (copy it before the next block)."""
+    def buffer(self, name: str, stream=None):
+        """Current-block intermediate copied into a new [nch][len] tensor (on `stream`, which is then
+        synchronised; the default is the legacy null stream, which waits for every blocking stream
+        -- never use it while a persistent PLL launch still waits for blocks)."""
         import torch
         p, s, n = C.c_void_p(), C.c_size_t(), C.c_int()
         check(lib().sdr_ctx_buffer(self._h, name.encode(), C.byref(p), C.byref(s), C.byref(n)), "sdr_ctx_buffer")
@@ -359,9 +361,17 @@ class Pipeline:
         out = torch.empty(self.nch, n.value, dtype=torch.float32, device=self.torch_device)
         import ctypes
         hip = _hip()
-        rc = hip.hipMemcpy2D(ctypes.c_void_p(out.data_ptr()), ctypes.c_size_t(4 * n.value), p,
-                             ctypes.c_size_t(4 * s.value), ctypes.c_size_t(4 * n.value), ctypes.c_size_t(self.nch),
-                             ctypes.c_int(3))
+        st = _stream(stream) if stream is not None else None
+        if st is None:
+            rc = hip.hipMemcpy2D(ctypes.c_void_p(out.data_ptr()), ctypes.c_size_t(4 * n.value), p,
+                                 ctypes.c_size_t(4 * s.value), ctypes.c_size_t(4 * n.value),
+                                 ctypes.c_size_t(self.nch), ctypes.c_int(3))
+        else:
+            rc = hip.hipMemcpy2DAsync(ctypes.c_void_p(out.data_ptr()), ctypes.c_size_t(4 * n.value), p,
+                                      ctypes.c_size_t(4 * s.value), ctypes.c_size_t(4 * n.value),
+                                      ctypes.c_size_t(self.nch), ctypes.c_int(3), ctypes.c_void_p(st))
+            if rc == 0:
+                rc = hip.hipStreamSynchronize(ctypes.c_void_p(st))
         if rc != 0:
             raise SdrError(f"hipMemcpy2D failed ({rc})")
         del full
@@ -384,4 +394,6 @@ def _hip():
         if _hiplib is None:
             raise SdrError("libamdhip64.so not found")
         _hiplib.hipMemcpy2D.restype = C.c_int
+        _hiplib.hipMemcpy2DAsync.restype = C.c_int
+        _hiplib.hipStreamSynchronize.restype = C.c_int
     return _hiplib

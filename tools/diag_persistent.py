@@ -43,13 +43,15 @@ for split in splits:
         pipe.stereo_post(lr, stream=s_post)
         pipe.rds_post(None, bits=False, stream=s_post)
         s_post.synchronize()
-        car = pipe.buffer("carrier").cpu().numpy(); ip = pipe.buffer("ipll").cpu().numpy()
+        with torch.cuda.stream(s_post):
+            lrh = lr.cpu().numpy()
+        car = pipe.buffer("carrier", stream=s_post).cpu().numpy()
+        ip = pipe.buffer("ipll", stream=s_post).cpu().numpy()
         ok = [np.array_equal(car.view(np.uint32), want[b][0].view(np.uint32)),
               np.array_equal(ip.view(np.uint32), want[b][1].view(np.uint32)),
-              np.array_equal(lr.cpu().numpy(), want[b][2])]
+              np.array_equal(lrh, want[b][2])]
         first = int(np.argmax(car.view(np.uint32)[0] != want[b][0].view(np.uint32)[0])) if not ok[0] else -1
         res.append(("ok" if all(ok) else f"BAD{ok} first-carrier-diff@{first}"))
-    torch.cuda.synchronize()
     print(split, pipe.plls_report(stream=s_pll)[:3], res, flush=True)
     bench.destroy_masked_streams(torch, pkg, torch.device("cuda", 0), created)
     pipe.close()
