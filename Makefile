@@ -1,6 +1,7 @@
 # Build everything in-tree (the .so files travel to the GPU box with the snapshot).
 #   make            libsdr_amd.so (HIP kernels + C ABI, gfx950), libsdr_host.so (the reference's
 #                   C++ stage/primitive API over the C ABI), bin/sdr_project (the receiver CLI),
+#                   bin/sdr_multi (the multi-channel receiver),
 #                   oracle/liboracle.so (+ oracle/_ref when the reference tree is present here)
 HIPCC    ?= /opt/rocm/bin/hipcc
 CXX      ?= g++
@@ -21,12 +22,13 @@ HOSTLIB   := $(PKG)/libsdr_host.so
 HOSTSRCS  := $(PKG)/host/dropin_primitives.cpp $(PKG)/host/dropin_stages.cpp $(PKG)/host/rds_frame.cpp
 HOSTHDRS  := $(wildcard include/dropin/*.h) $(PKG)/host/hip_util.h include/sdr_amd.h
 CLI       := $(PKG)/bin/sdr_project
+MULTI     := $(PKG)/bin/sdr_multi
 
 .PHONY: all lib host oracle clean
 all: lib host oracle
 
 lib: $(LIB)
-host: $(HOSTLIB) $(CLI)
+host: $(HOSTLIB) $(CLI) $(MULTI)
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,libsdr_amd.so -o $@ $(SRCS)
@@ -39,9 +41,14 @@ $(CLI): $(PKG)/host/sdr_project.cpp $(HOSTLIB)
 	@mkdir -p $(dir $@)
 	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -lsdr_host -Wl,-rpath,'$$ORIGIN/..'
 
+$(MULTI): $(PKG)/host/sdr_multi.cpp include/dropin/fm_batch.h $(HOSTLIB)
+	@mkdir -p $(dir $@)
+	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -lsdr_host -lsdr_amd -L$(ROCM)/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/..' -Wl,-rpath,$(ROCM)/lib
+
 oracle: host
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIB) $(HOSTLIB) $(CLI)
+	rm -f $(LIB) $(HOSTLIB) $(CLI) $(MULTI)
 	$(MAKE) -C oracle clean

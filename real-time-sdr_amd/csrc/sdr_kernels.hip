@@ -2726,7 +2726,10 @@ int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, 
     for (int j = 0; j < n && block_ms; j++)   // s_memrealtime: 100 MHz
         block_ms[j] = (t1[j] >= t0[j]) ? (double)(t1[j] - t0[j]) * 1e-5 : -1.0;
     if (nblocks) *nblocks = n;
-    if (words[2]) return fail(SDR_E_HIP, "plls_report: a persistent PLL wait timed out (outputs invalid)");
+    if (words[2])
+        return fail(SDR_E_HIP, "plls_report: a persistent PLL wait timed out (outputs invalid): err %u, flag %u, "
+                    "done %u, signalled %u, launched %u, waves %u", words[2], words[0], words[1], c->pers_signaled,
+                    c->pers_launched, c->pers_waves);
     return SDR_OK;
 }
 

@@ -89,3 +89,16 @@ def test_rds_frame_layer_matches_reference_text(golden_long, tmp_path):
         r = subprocess.run([str(exe)], input=feed, capture_output=True, text=True, check=True, timeout=60)
         assert r.stderr == fx["rds_text"], f"channel {ch}"
         assert "Program Service: MI355X" in r.stderr
+
+
+def test_fm_batch_queue_protocol(tmp_path):
+    """ThreadSafeQueue<FmBatch*> (the device-resident queue payload, include/dropin/fm_batch.h): the
+    reference's push / wait_and_pop / prepare protocol with 2 recycled batches, 1 producer and 2
+    consumers over 20000 payloads -- in order, each once per consumer, never reissued early."""
+    import subprocess
+    exe = tmp_path / "fmq"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    "-I", str(ROOT / "include" / "dropin"), str(ROOT / "tests/cpp/fm_batch_queue_test.cpp"),
+                    "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr

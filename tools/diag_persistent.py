@@ -5,6 +5,8 @@ splits given on the command line, e.g. `python tools/diag_persistent.py 5,9 14,0
 import pathlib
 import sys
 
+import time
+
 import numpy as np
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
@@ -33,6 +35,7 @@ for split in splits:
     lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
     starts = np.cumsum([0] + split[:-1])
     res = []
+    T0 = time.time()
     for b in range(nb):
         if b in starts:
             pipe.plls_launch(split[list(starts).index(b)], stream=s_pll)
@@ -52,6 +55,11 @@ for split in splits:
               np.array_equal(lrh, want[b][2])]
         first = int(np.argmax(car.view(np.uint32)[0] != want[b][0].view(np.uint32)[0])) if not ok[0] else -1
         res.append(("ok" if all(ok) else f"BAD{ok} first-carrier-diff@{first}"))
-    print(split, pipe.plls_report(stream=s_pll)[:3], res, flush=True)
+        print(f"  block {b}: {res[-1]} at {time.time() - T0:.2f} s", flush=True)
+    print(split, res, flush=True)
+    try:
+        print("  report", pipe.plls_report(stream=s_pll)[:3], flush=True)
+    except Exception as e:  # noqa: BLE001
+        print("  report:", e, flush=True)
     bench.destroy_masked_streams(torch, pkg, torch.device("cuda", 0), created)
     pipe.close()
