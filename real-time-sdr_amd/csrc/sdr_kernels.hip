@@ -1437,7 +1437,7 @@ constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrea
 
 template <bool VEC>
 __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
-                                                  int first_parity, const uint32_t* pre_flag, uint32_t pre_first,
+                                                  const uint32_t* pre_flag, uint32_t pre_first,
                                                   uint32_t* done_count, uint32_t* err,
                                                   unsigned long long* t_start, unsigned long long* t_end,
                                                   int sys_acquire) {
@@ -1447,7 +1447,7 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
     __builtin_amdgcn_s_setprio(3);
     bool dead = false;
     for (int j = 0; j < nblocks; j++) {
-        const PllJob& jb = jobs.p[(first_parity + j) & 1].j[blockIdx.y];
+        const PllJob& jb = jobs.p[j & 1].j[blockIdx.y];   // p[0]: the parity of the launch's first block
         if (!dead) {
             const uint32_t want = pre_first + (uint32_t)j + 1u;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -2651,7 +2651,7 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     HIP_TRY(hipMemsetAsync(c->pers_t1, 0, (size_t)nblocks * sizeof(unsigned long long), s));
     const int n = c->info.block_if, nch = c->nch;
     PllJobs2 jobs{};
-    const int first_parity = c->parity ^ 1;   // the parity the next sdr_frontend switches to
+    const int first_parity = c->parity ^ 1;   // the parity the next sdr_frontend switches to: p[0]
     for (int k = 0; k < 2; k++) {
         const int saved = c->parity;
         c->parity = first_parity ^ k;
@@ -2676,10 +2676,10 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     uint32_t* w = c->pers_words;
     if (vec)
         hipLaunchKernelGGL(k_pll_multi<true>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
-                           first_parity, w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1, sys_acq);
+                           w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1, sys_acq);
     else
         hipLaunchKernelGGL(k_pll_multi<false>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
-                           first_parity, w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1, sys_acq);
+                           w, c->pers_launched, w + 1, w + 2, c->pers_t0, c->pers_t1, sys_acq);
     LAUNCH_CHECK();
     c->pers_launched += (uint32_t)nblocks;
     c->pers_last_n = nblocks;
