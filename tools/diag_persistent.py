@@ -30,8 +30,8 @@ for b in range(nb):
     want.append((ref.buffer("carrier").cpu().numpy(), ref.buffer("ipll").cpu().numpy(), lr.cpu().numpy()))
 for split in splits:
     pipe = pkg.Pipeline(nch)
-    created = []
-    s_fe, s_pll, s_post = bench.cu_masked_streams(torch, pkg, torch.device("cuda", 0), "64", created)
+    created = []   # non-blocking torch streams: the legacy null stream never waits on the PLL stream
+    s_fe, s_pll, s_post = (torch.cuda.Stream() for _ in range(3))
     lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
     starts = np.cumsum([0] + split[:-1])
     res = []
