@@ -151,7 +151,10 @@ int sdr_plls(sdr_ctx *ctx, void *stream);
  * waits for each block's signal (a device flag written in stream order), runs both PLLs, and
  * releases the waiting stream; a wait longer than 5 s ends the launch without computing and is
  * reported by sdr_plls_report, which also returns each block's PLL time of the last launch (ms,
- * from the device clock) and synchronises `stream`. Not with SDR_FLAG_PLL_LIBM. */
+ * from the device clock: its last wave's end minus the later of its signal and the previous
+ * block's end) and synchronises `stream`. While a launch still waits for blocks, nothing may
+ * synchronise with the PLL stream implicitly: a CU-masked stream is a blocking stream, so work on
+ * the legacy null stream would wait for it (until the 5 s bound). Not with SDR_FLAG_PLL_LIBM. */
 int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
 int sdr_plls_signal(sdr_ctx *ctx, void *stream);
 int sdr_plls_wait(sdr_ctx *ctx, void *stream);

@@ -2723,8 +2723,13 @@ int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, 
         HIP_TRY(hipMemcpyAsync(t1.data(), c->pers_t1, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
-    for (int j = 0; j < n && block_ms; j++)   // s_memrealtime: 100 MHz
-        block_ms[j] = (t1[j] >= t0[j]) ? (double)(t1[j] - t0[j]) * 1e-5 : -1.0;
+    // block j's PLL time: from when both its input was signalled and the previous block was done
+    // (waves drift apart, so the first wave's start can precede the slowest wave's previous end)
+    // to its last wave's end, from the 100 MHz s_memrealtime stamps
+    for (int j = 0; j < n && block_ms; j++) {
+        const unsigned long long from = j > 0 ? std::max(t0[j], t1[j - 1]) : t0[j];
+        block_ms[j] = (t1[j] >= from) ? (double)(t1[j] - from) * 1e-5 : -1.0;
+    }
     if (nblocks) *nblocks = n;
     if (words[2])
         return fail(SDR_E_HIP, "plls_report: a persistent PLL wait timed out (outputs invalid): err %u, flag %u, "
