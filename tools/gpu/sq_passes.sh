@@ -1,13 +1,13 @@
 # SQ counter passes (one rocprofv3 --pmc run per group, each under its own time limit) over a
 # command; prints the per-kernel averages of kernels matching FILTER.
 #   TAG=x FILTER=k_pll CMD="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-isolated" \
-#   GROUPS="SQ_WAVES SQ_WAVE_CYCLES ...;SQ_WAVES SQ_WAIT_ANY ..." bash tools/gpu/sq_passes.sh
+#   PASSES="SQ_WAVES SQ_WAVE_CYCLES ...;SQ_WAVES SQ_WAIT_ANY ..." bash tools/gpu/sq_passes.sh
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-sq}
 mkdir -p $O
 i=0
-IFS=';' read -ra G <<< "$GROUPS"
+IFS=";" read -ra G <<< "$PASSES"
 for grp in "${G[@]}"; do
   i=$((i+1))
   echo "[pass $i] $grp"
