@@ -1332,37 +1332,6 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
             }
         }
     };
-    // one chunk from register buffer u (fast path, redone with checked steps if a proof fails)
-    auto run_chunk = [&](float* xbu, double* rbu, int i0) {
-        double wv[C];
-        if (TAB) {
-#pragma unroll
-            for (int k = 0; k < C / 2; k++) {
-                const double2 v = reinterpret_cast<const double2*>(wtab + i0)[k];
-                wv[2 * k] = v.x; wv[2 * k + 1] = v.y;
-            }
-        }
-        const PllRegs snap = r;
-        PllProof pf;
-        float tv[C];
-#pragma unroll
-        for (int j = 0; j < C; j++)
-            pll_step<false, TAB>(r, xbu[j], rbu[j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
-        if (!pll_chunk_ok<TAB>(pf, r, w, C)) {
-            r = snap;
-#pragma unroll
-            for (int j = 0; j < C; j++)
-                pll_step<true, TAB>(r, xbu[j], rbu[j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
-        }
-        if (VEC) {
-#pragma unroll
-            for (int k = 0; k < C / 4; k++)
-                reinterpret_cast<float4*>(tb + i0)[k] = make_float4(tv[4 * k], tv[4 * k + 1], tv[4 * k + 2], tv[4 * k + 3]);
-        } else {
-#pragma unroll
-            for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
-        }
-    };
     if (nmain > 0) {
 #pragma unroll
         for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
@@ -1370,36 +1339,66 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
     for (int c0 = 0; c0 < nmain; c0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; u++) {
-            run_chunk(xb[u], rb[u], (c0 + u) * C);
-            // refill with the chunk NB ahead; the last refills re-read the final full chunk
-            // (harmless, keeps the loop branch-free), so the chunks past the main loop are loaded
-            load_chunk(xb[u], rb[u], min(c0 + u + NB, nchunks - 1) * C);
+            const int i0 = (c0 + u) * C;
+            double wv[C];
+            if (TAB) {
+#pragma unroll
+                for (int k = 0; k < C / 2; k++) {
+                    const double2 v = reinterpret_cast<const double2*>(wtab + i0)[k];
+                    wv[2 * k] = v.x; wv[2 * k + 1] = v.y;
+                }
+            }
+            const PllRegs snap = r;
+            PllProof pf;
+            float tv[C];
+#pragma unroll
+            for (int j = 0; j < C; j++)
+                pll_step<false, TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
+            if (!pll_chunk_ok<TAB>(pf, r, w, C)) {
+                r = snap;
+#pragma unroll
+                for (int j = 0; j < C; j++)
+                    pll_step<true, TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
+            }
+            if (VEC) {
+#pragma unroll
+                for (int k = 0; k < C / 4; k++)
+                    reinterpret_cast<float4*>(tb + i0)[k] = make_float4(tv[4 * k], tv[4 * k + 1], tv[4 * k + 2], tv[4 * k + 3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
+            }
+            // refill (the last refills re-read the final chunk: harmless, keeps the loop branch-free)
+            load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
         }
     }
-    // the full chunks past the last multiple of NB (their inputs are in buffers 0.., see above)
-#pragma unroll
-    for (int u = 0; u < NB - 1; u++)
-        if (nmain > 0 && nmain + u < nchunks) run_chunk(xb[u], rb[u], (nmain + u) * C);
     {
-        // the last n % C steps, checked, with their inputs loaded together up front (one memory
-        // latency for the tail instead of one per step)
-        const int i0 = (nmain > 0 ? nchunks : 0) * C;
-        float xt[C];
-        double rt[C], wt[C];
-#pragma unroll
-        for (int k = 0; k < C; k++) {
-            if (i0 + k < n) {
-                xt[k] = x[i0 + k];
-                rt[k] = rxp[i0 + k];
-                wt[k] = TAB ? wtab[i0 + k] : 0.0;
-            }
-        }
+        // the rest (< NB chunks + n % C steps), checked, from register buffers loaded one piece
+        // ahead (one exposed memory latency for the whole rest instead of one per step)
         PllProof pf;
+        const int i_rest = nmain * C;
+        float xr[C];
+        double rr[C], wr[C];
+        auto load_rest = [&](int i0) {
 #pragma unroll
-        for (int k = 0; k < C; k++)
-            if (i0 + k < n) pll_step<true, TAB>(r, xt[k], rt[k], Kp, Ki, w, wt[k], tb[i0 + k], pf);
-        for (int i = i0 + C; i < n; i++)   // only when nmain == 0 (n < NB * C)
-            pll_step<true, TAB>(r, x[i], rxp[i], Kp, Ki, w, TAB ? wtab[i] : 0.0, tb[i], pf);
+            for (int k = 0; k < C; k++) {
+                const int i = min(i0 + k, n - 1);
+                xr[k] = x[i];
+                rr[k] = rxp[i];
+                wr[k] = TAB ? wtab[i] : 0.0;
+            }
+        };
+        if (i_rest < n) load_rest(i_rest);
+        for (int i0 = i_rest; i0 < n; i0 += C) {
+            float xc[C];
+            double rc[C], wc[C];
+#pragma unroll
+            for (int k = 0; k < C; k++) { xc[k] = xr[k]; rc[k] = rr[k]; wc[k] = wr[k]; }
+            if (i0 + C < n) load_rest(i0 + C);
+#pragma unroll
+            for (int k = 0; k < C; k++)
+                if (i0 + k < n) pll_step<true, TAB>(r, xc[k], rc[k], Kp, Ki, w, wc[k], tb[i0 + k], pf);
+        }
     }
     if (TAB) r.toff = s0.trigOffset + (double)n;               // pll.cpp:46, n times (exact)
     // every field but lastCarrier (k_nco_out's); the feedback back in the frame of t
