@@ -1271,6 +1271,9 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
 #define SDR_PLL_CHUNK 16
 #endif
 constexpr int PLL_CHUNK = SDR_PLL_CHUNK;
+#ifndef SDR_PLL_W01
+#define SDR_PLL_W01 1
+#endif
 #ifndef SDR_PLL_NBUF
 #define SDR_PLL_NBUF 2
 #endif
@@ -1336,14 +1339,25 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
 #pragma unroll
         for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
     }
+#if SDR_PLL_W01
+    double2 w01 = TAB ? reinterpret_cast<const double2*>(wtab)[0] : double2{0.0, 0.0};
+#endif
     for (int c0 = 0; c0 < nmain; c0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; u++) {
             const int i0 = (c0 + u) * C;
             double wv[C];
             if (TAB) {
+                // the first two steps' table entries were read at the end of the previous chunk
+                // (w01), so the chunk's first steps do not wait on the LDS latency
+#if SDR_PLL_W01
+                wv[0] = w01.x; wv[1] = w01.y;
+#pragma unroll
+                for (int k = 1; k < C / 2; k++) {
+#else
 #pragma unroll
                 for (int k = 0; k < C / 2; k++) {
+#endif
                     const double2 v = reinterpret_cast<const double2*>(wtab + i0)[k];
                     wv[2 * k] = v.x; wv[2 * k + 1] = v.y;
                 }
@@ -1370,6 +1384,9 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
             }
             // refill (the last refills re-read the final chunk: harmless, keeps the loop branch-free)
             load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
+#if SDR_PLL_W01
+            if (TAB) w01 = reinterpret_cast<const double2*>(wtab)[min(i0 + C, n - 2) >> 1];
+#endif
         }
     }
     {
