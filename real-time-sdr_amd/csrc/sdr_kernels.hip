@@ -1272,7 +1272,7 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
 #endif
 constexpr int PLL_CHUNK = SDR_PLL_CHUNK;
 #ifndef SDR_PLL_W01
-#define SDR_PLL_W01 1
+#define SDR_PLL_W01 0
 #endif
 #ifndef SDR_PLL_NBUF
 #define SDR_PLL_NBUF 2
