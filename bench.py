@@ -37,6 +37,7 @@ import numpy as np
 
 ROOT = pathlib.Path(__file__).resolve().parent
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP32_VECTOR_PEAK_TF = 157.3     # MI355X FP32 vector (packed) peak, TFLOP/s
 METRIC = "IQ MSamples/s/node (mono+stereo+RDS), 1/2/4/8 GPU; HBM GB/s %peak"
 VERIFY_CHANNELS = 8             # channels of rank 0 whose outputs are checked after the timed run
 
@@ -304,8 +305,39 @@ class GpuStepper:
                          "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(nch, name),
                          "avg_launch_ms": round(ms, 4)}
+            if not flags:
+                # exact mode is VALU-bound (f32 multiply and add per tap, no FMA): the same time
+                # against the f32 vector peak (report the VALU fraction too)
+                flops = nch * info.block_if * 2 * info.rf_taps * 2
+                res[name]["valu"] = {"achieved_tflops": round(flops / (ms / 1e3) / 1e12, 2),
+                                     "peak_tflops": FP32_VECTOR_PEAK_TF,
+                                     "frac": round(flops / (ms / 1e3) / 1e12 / FP32_VECTOR_PEAK_TF, 4)}
             p2.close()
+        res["hbm_copy"] = self.copy_bandwidth()
         return res
+
+    def copy_bandwidth(self, nbytes: int = 1 << 31, reps: int = 10) -> dict:
+        """Device-to-device copy of a 2 GiB buffer (read + write bytes / time): the HBM bandwidth a
+        plain streaming kernel reaches on this box, next to the nominal 8 TB/s peak."""
+        torch = self.torch
+        a = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        b = torch.empty_like(a)
+        s2 = torch.cuda.Stream(self.dev)
+        with torch.cuda.stream(s2):
+            a.fill_(1)
+            for _ in range(2):
+                b.copy_(a)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s2)
+            for _ in range(reps):
+                b.copy_(a)
+            e1.record(s2)
+        torch.cuda.synchronize(self.dev)
+        ms = e0.elapsed_time(e1) / reps
+        del a, b
+        return {"kernel": "torch copy_ (device to device)", "bytes": 2 * nbytes,
+                "achieved": round(2 * nbytes / (ms / 1e3) / 1e9, 1), "unit": "GB/s",
+                "frac_of_peak": round(2 * nbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
 
     def captured(self) -> dict:
         """Host copies of the inputs and captured outputs of the checked channels."""

@@ -47,6 +47,12 @@ constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-
 // relative error of cos on |r| <= pi/4 by tools/pllmath/fit_poly.py: 2^-51.7 in double evaluation
 constexpr double C1 = 0.04166666666659653, C2 = -0.0013888888877611482, C3 = 2.4801580707202765e-05,
                  C4 = -2.755552309095219e-07, C5 = 2.0645117778725974e-09;
+// sin kernel of the k_pll step (sincos_kernels): degree-4 P, refitted the same way (fit_poly.py):
+// 2^-47.48 relative error in double Horner evaluation on |r| <= pi/4 -- 46 f64 ulps at most, inside
+// the tie test's 128-ulp margin, and 0.5 (eps_s + eps_c) < 2^-48.3 of phase-detector error, inside
+// EPS_ABS_E2 with the 2^-45.9 of the Y * rx substitution
+constexpr double SR1 = -0.1666666666663035, SR2 = 0.008333333325077597, SR3 = -0.00019841263728549816,
+                 SR4 = 2.755533964014372e-06, SR5 = -2.4760453463432028e-08;
 // error bounds used by the rounding test (generous: measured errors are far smaller)
 constexpr double EPS_ABS_E = 0x1p-45;      // absolute, phase detector output (|e| <= pi)
 constexpr double T_MAX = 0x1p30;           // reduction valid below this
@@ -310,7 +316,8 @@ PLLM_HD SinCosR sincos_r(float t) {
 //  * sincos_rn: the reduction rounds -t (2/pi) against MAGIC + 1, so the low word of the rounded
 //    value is nq1 = 1 - q (mod 2^32) -- exactly what base_angle needs -- and kdn = -kd folds its
 //    sign into the two reduction fmas. PLL_POLY = 1 evaluates both kernels by Horner (2
-//    multiplies fewer than Estrin's z^2, z^4 powers, a longer dependent chain), 0 by Estrin.
+//    multiplies fewer than Estrin's z^2, z^4 powers, a longer dependent chain) with the refitted
+//    5-coefficient sin (SR1..SR5, one fma fewer than fdlibm's), 0 by Estrin with fdlibm's sin.
 //  * base_angle_n(nlo, nq1, b, mr) = base_angle(nlo, 1 - nq1, b, mr): one 3-input add.
 // ------------------------------------------------------------------------------------------
 #ifndef PLL_POLY
@@ -319,21 +326,30 @@ PLLM_HD SinCosR sincos_r(float t) {
 constexpr double MAGIC1 = 6755399441055745.0;   // 1.5 * 2^52 + 1
 
 struct SinCosRN {
-    double cr, sr;   // cos r, sin r (relative error < 2^-50)
+    double cr, sr;   // cos r, sin r (relative error < 2^-51.7, 2^-47.4 with PLL_POLY 1)
     double r;        // t - q pi/2 in [-pi/4, pi/4]
     uint32_t nq1;    // 1 - q (mod 2^32)
     uint32_t b;      // [r < 0]
     uint32_t tie;    // min(tie_key64(cr), tie_key64(sr)); the roundings are safe iff tie > TIE_MIN
+    uint32_t tc, ts; // the two keys
 };
 
 PLLM_HD void sincos_kernels(double r, double& cr, double& sr) {
     const double z = r * r;
-#if PLL_POLY
-    double sp = fma_(z, S6, S5);
-    sp = fma_(z, sp, S4);
-    sp = fma_(z, sp, S3);
-    sp = fma_(z, sp, S2);
-    sp = fma_(z, sp, S1);
+#if PLL_POLY == 2
+    // two-level: P = (a0 + z a1) + z^2 ((a2 + z a3) + z^2 a4) -- one multiply (z^2) more than
+    // Horner, 4 dependent operations after z instead of 6 (cos) / 5 (sin); 2^-47.48 (sin),
+    // 2^-51.79 (cos) relative in double evaluation
+    const double z2 = z * z;
+    const double sp = fma_(z2, fma_(z2, SR5, fma_(z, SR4, SR3)), fma_(z, SR2, SR1));
+    const double cq = fma_(z2, fma_(z2, C5, fma_(z, C4, C3)), fma_(z, C2, C1));
+    sr = fma_(r * z, sp, r);
+    cr = fma_(z2, cq, fma_(z, -0.5, 1.0));
+#elif PLL_POLY
+    double sp = fma_(z, SR5, SR4);
+    sp = fma_(z, sp, SR3);
+    sp = fma_(z, sp, SR2);
+    sp = fma_(z, sp, SR1);
     double cp = fma_(z, C5, C4);
     cp = fma_(z, cp, C3);
     cp = fma_(z, cp, C2);
@@ -362,8 +378,9 @@ PLLM_HD SinCosRN sincos_rn(float t) {
     o.r = r;
     o.nq1 = (uint32_t)__builtin_bit_cast(uint64_t, kdp);
     o.b = (uint32_t)(__builtin_bit_cast(uint64_t, r) >> 63);
-    const uint32_t tc = tie_key64(o.cr), ts = tie_key64(o.sr);
-    o.tie = tc < ts ? tc : ts;
+    o.tc = tie_key64(o.cr);
+    o.ts = tie_key64(o.sr);
+    o.tie = o.tc < o.ts ? o.tc : o.ts;
     return o;
 }
 

@@ -1112,7 +1112,8 @@ struct PllJobs {
 };
 
 struct PllRegs {
-    float fbI, fbQ, integ, ph;   // fbI, fbQ in the reduced frame: RN(cos r), RN(sin r) (pll_math.h)
+    float fbI, fbQ;              // in the reduced frame: RN(cos r), RN(sin r) (pll_math.h)
+    f32x2 ip;                    // {integrator, phaseEst}: one packed multiply and add per step
     double toff;
     double c, s, mr;             // f64 cos r, sin r and -r of the previous step's t = q pi/2 + r
     uint32_t nq1, b;             // 1 - q (mod 2^32) for its quadrant q, and [r < 0]
@@ -1126,10 +1127,9 @@ struct PllRegs {
 // chunk is redone with libm fallbacks, which use the state's feedback exactly.
 __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
     PllRegs r;
-    r.integ = st.integrator;
-    r.ph = st.phaseEst;
+    r.ip = f32x2{st.integrator, st.phaseEst};
     r.toff = st.trigOffset;
-    const float t_prev = (float)(w * r.toff + (double)r.ph);
+    const float t_prev = (float)(w * r.toff + (double)r.ip.y);
     const pllm::SinCosRN sc = pllm::sincos_rn(t_prev);
     float fI = (float)sc.cr, fQ = (float)sc.sr;
     pllm::rot_q(1u - sc.nq1, fI, fQ);
@@ -1170,13 +1170,18 @@ struct PllProof {
     uint32_t tie = ~0u;
     float tmax = 0.0f;
 };
+#ifndef SDR_PLL_EDHI
+#define SDR_PLL_EDHI 0
+#endif
+// |e| bound of the fast phase detector (the wrap to [-pi, pi] is the reference's below it)
+constexpr double PLL_EMAX = SDR_PLL_EDHI ? pllm::PI - 0x1p-30 - 0x1p-42 : pllm::PI - 0x1p-30;
 constexpr double PLL_TAB_WT_MAX = 0x1.6p29;   // |w * trigOffset| bound of the table path (above)
 
 // TAB: the trigArg offsets come from a table whose range the kernel checked once (pll_run)
 template <bool TAB>
 __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
-    return (pf.emax < pllm::PI - 0x1p-30) & (pf.split == 0u) & (pf.tie > pllm::TIE_MIN) &
-           (__builtin_fabs(r.ph) < 0x1p28f) & (__builtin_fabs(r.integ) < 0x1p20f) &
+    return (pf.emax < PLL_EMAX) & (pf.split == 0u) & (pf.tie > pllm::TIE_MIN) &
+           (__builtin_fabs(r.ip.y) < 0x1p28f) & (__builtin_fabs(r.ip.x) < 0x1p20f) &
            (TAB || (pf.tmax < 0x1p30f));
 }
 
@@ -1205,6 +1210,14 @@ __device__ __forceinline__ uint32_t or_xor(uint32_t acc, uint32_t lo, uint32_t h
     return d;
 }
 
+// tie accumulator: min(acc, tc, ts) as one v_min3_u32 (the compiler otherwise pairs the keys of
+// consecutive steps into a v_min_u32 + v_min3_u32 tree)
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 // One step of pll.cpp:36-50. CHECKED: every result the fast path cannot prove is recomputed
 // with the f64 libm exactly as the reference (used for chunk redo and short tails).
 template <bool CHECKED, bool TAB>
@@ -1218,11 +1231,19 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
     // pll.cpp:39: atan2(eQ, eI) = base + Y/X (pll_math.h phase_detect2), rounding proven below
     const double base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
     const double Y = pllm::fma_((double)eI0, r.s, (double)eQ0 * r.c);
+#if SDR_PLL_EDHI
+    // the bracket ed -/+ eps as fma(Y, rx, base -/+ eps): base -/+ eps is ready before the input,
+    // so the rounded e is one operation closer to Y (same proof: each end moves < 2^-50.5, far
+    // inside eps - |error of ed|); |ed| <= |ed + eps| + 2^-43 for the range test
+    const double ed = pllm::fma_(Y, rx, base + pllm::EPS_ABS_E2);
+    const float lo = (float)pllm::fma_(Y, rx, base - pllm::EPS_ABS_E2), hi = (float)ed;
+#else
     const double ed = pllm::fma_(Y, rx, base);
     const float lo = (float)(ed - pllm::EPS_ABS_E2), hi = (float)(ed + pllm::EPS_ABS_E2);
+#endif
     float e = hi;                                             // = RN32(ed) whenever lo == hi
     if (CHECKED) {
-        if (!((__builtin_fabs(ed) < pllm::PI - 0x1p-30) && lo == hi)) {
+        if (!((__builtin_fabs(ed) < PLL_EMAX) && lo == hi)) {
             float a = eI0, b = -eQ0;                          // eI - i eQ = i^q (eI0 - i eQ0)
             pllm::rot_q(1u - r.nq1, a, b);
             e = pll_atan2_ref(-b, a);                         // pll.cpp:39
@@ -1231,14 +1252,18 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
         pf.emax = fmax(pf.emax, __builtin_fabs(ed));
         pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
     }
-    r.integ = r.integ + Ki * e;                               // pll.cpp:41
-    r.ph = r.ph + Kp * e + r.integ;                           // pll.cpp:42
+    // pll.cpp:41-42: integ += Ki e; phaseEst = (phaseEst + Kp e) + integ, with the two products
+    // and the two first sums as one v_pk_mul_f32 + one v_pk_add_f32 (the same f32 roundings)
+    r.ip = r.ip + f32x2{Ki, Kp} * f32x2{e, e};
+    float ph = r.ip.y;                                        // in place (else a pk_add + move)
+    asm("v_add_f32 %0, %0, %1" : "+v"(ph) : "v"(r.ip.x));
+    r.ip.y = ph;
     float t;
     if (TAB) {                                                // wt = w * trigOffset, tabulated
-        t = (float)(wt + (double)r.ph);                       // pll.cpp:47
+        t = (float)(wt + (double)r.ip.y);                     // pll.cpp:47
     } else {
         r.toff += 1.0;                                        // pll.cpp:46
-        t = (float)(w * r.toff + (double)r.ph);               // pll.cpp:47
+        t = (float)(w * r.toff + (double)r.ip.y);             // pll.cpp:47
     }
     const pllm::SinCosRN sc = pllm::sincos_rn(t);
     r.c = sc.cr;
@@ -1261,7 +1286,7 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
             if (!in_range) r.mr = __builtin_nan("");
         }
     } else {
-        pf.tie = min(pf.tie, sc.tie);
+        pf.tie = min3_u32(pf.tie, sc.tc, sc.ts);
         if (!TAB) pf.tmax = fmaxf(pf.tmax, __builtin_fabsf(t));
     }
     t_out = t;
@@ -1422,8 +1447,8 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
     pllm::rot_q(1u - r.nq1, r.fbI, r.fbQ);
     st[ch].feedbackI = r.fbI;
     st[ch].feedbackQ = r.fbQ;
-    st[ch].integrator = r.integ;
-    st[ch].phaseEst = r.ph;
+    st[ch].integrator = r.ip.x;
+    st[ch].phaseEst = r.ip.y;
     st[ch].trigOffset = r.toff;
 }
 

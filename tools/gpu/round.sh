@@ -24,6 +24,7 @@ if [ "${PROF:-1}" = 1 ]; then
       python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-isolated ${BENCH_ARGS:-} > $O/prof.log 2>&1; rc=$?
   [ $rc -eq 0 ] || { tail -20 $O/prof.log; exit $rc; }
   find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+  rm -rf $O/prof   # raw traces: gpurun_out/ is only copied back below 64 MiB
   head -14 $O/kernel_stats.csv | cut -c1-160
 fi
 if [ "${PMC:-1}" = 1 ]; then
@@ -33,6 +34,7 @@ if [ "${PMC:-1}" = 1 ]; then
         python3 tools/bench_frontend.py --iters 10 > $O/pmc_$c.log 2>&1; rc=$?
     [ $rc -eq 0 ] || { tail -20 $O/pmc_$c.log; exit $rc; }
     find $O/pmc_$c -name "*counter_collection.csv" -exec cp {} $O/pmc_$c.csv \;
+    rm -rf $O/pmc_$c
   done
   timeout -k 10 60 python tools/pmc_summary.py $O 1024 > $O/pmc_summary.json; cat $O/pmc_summary.json
 fi
@@ -42,10 +44,13 @@ if [ "${PLLPMC:-1}" = 1 ]; then
              "SQ_WAVES SQ_WAIT_ANY SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_SALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64"; do
     i=$((i+1))
     step pll pmc $i
-    timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $O/pllpmc$i -o b -- \
+    # per-block dispatch: PMC collection serialises dispatches, which the persistent PLL (waiting
+    # on flags set by later dispatches) cannot survive
+    SDR_BENCH_PLL=dispatch timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $O/pllpmc$i -o b -- \
         python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-isolated > $O/pllpmc$i.log 2>&1 || { tail -20 $O/pllpmc$i.log; exit 1; }
     f=$(find $O/pllpmc$i -name "*counter_collection.csv" | head -1)
     cp "$f" $O/pllpmc$i.csv
+    rm -rf $O/pllpmc$i
     python tools/sq_summary.py $O/pllpmc$i.csv k_pll
   done
 fi
