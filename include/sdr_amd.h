@@ -184,6 +184,11 @@ int sdr_ctx_buffer(sdr_ctx *ctx, const char *name, const float **ptr, size_t *st
 int sdr_stream_create_cu_range(void **stream, int device, int first_cu, int n_cu, int exclude);
 int sdr_stream_destroy(void *stream);
 
+/* Bandwidth calibration (no reference counterpart): device-to-device copy of `bytes` (a multiple
+ * of 16, 16-byte aligned pointers) with a streaming kernel over every CU, so that a benchmark can
+ * state the HBM rate a plain stream reaches next to the nominal peak. */
+int sdr_hbm_copy(void *dst, const void *src, size_t bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

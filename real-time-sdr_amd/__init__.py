@@ -93,6 +93,7 @@ def lib() -> C.CDLL:
         "sdr_plls_report": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32), vp], i32),
         "sdr_rds_post": ([vp, vp, sz, vp], i32),
         "sdr_ctx_buffer": ([vp, C.c_char_p, C.POINTER(vp), C.POINTER(sz), C.POINTER(i32)], i32),
+        "sdr_hbm_copy": ([vp, vp, sz, vp], i32),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -106,6 +107,15 @@ def check(rc: int, what: str = "") -> None:
     if rc != SDR_OK:
         msg = lib().sdr_last_error().decode(errors="replace")
         raise SdrError(f"{what} failed ({rc}): {msg}")
+
+
+def hbm_copy(dst, src, stream=None) -> None:
+    """dst <- src (same byte size, 16-byte aligned device tensors) with the calibration copy kernel
+    (sdr_hbm_copy): the HBM rate a plain stream reaches, for the benchmark's roofline context."""
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != nbytes:
+        raise SdrError("hbm_copy: size mismatch")
+    check(lib().sdr_hbm_copy(_ptr(dst), _ptr(src), nbytes, _stream(stream)), "sdr_hbm_copy")
 
 
 # ------------------------------------------------------------------ torch plumbing helpers

@@ -1907,6 +1907,16 @@ __global__ void k_fill_u8(uint8_t* p, uint8_t v, size_t n) {
     if (i < n) p[i] = v;
 }
 
+// Bandwidth calibration (sdr_hbm_copy): one 16-byte element per lane, one short-lived workgroup per
+// 4 KiB -- the fastest plain copy measured on this device (tools/hbm_copy_bench.hip: 6.2 TB/s, where
+// grid-stride loops with 1-8 loads in flight per lane reach 4.1-5.7) -- the HBM rate a plain stream
+// reaches, the practical ceiling the front end's roofline fraction is read against.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_hbm_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 
@@ -2281,6 +2291,19 @@ int sdr_stream_destroy(void* stream) {
     const int rc = release_stream_scratch((hipStream_t)stream);
     if (rc != SDR_OK) return rc;
     HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return SDR_OK;
+}
+
+int sdr_hbm_copy(void* dst, const void* src, size_t bytes, void* stream) {
+    if (!dst || !src || (bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) || (reinterpret_cast<uintptr_t>(src) & 15))
+        return fail(SDR_E_INVALID, "sdr_hbm_copy: pointers and size must be 16-byte aligned");
+    if (bytes == 0) return SDR_OK;
+    const size_t n = bytes / 16;
+    if ((n + 255) / 256 > 0x7FFFFFFFu) return fail(SDR_E_INVALID, "sdr_hbm_copy: %zu bytes is too large", bytes);
+    const int grid = (int)((n + 255) / 256);
+    hipLaunchKernelGGL(k_hbm_copy, dim3(grid), dim3(256), 0, S(stream), static_cast<u32x4*>(dst),
+                       static_cast<const u32x4*>(src), n);
+    HIP_TRY(hipGetLastError());
     return SDR_OK;
 }
 

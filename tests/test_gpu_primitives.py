@@ -250,3 +250,18 @@ def test_fmpll_long_stream_shared_offset(pkg, oracle, torch_cuda):
             o[-1] = 1.0
             oracle.fmpll(x[c], freq, 240000.0, o, refs[c], nco, 0.0, bw)
             assert np.array_equal(_u32(out[c]), _u32(o)), f"toff {toff:g} ch {c}"
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096 + 48, 3 * (1 << 20) + 16 * 7])
+def test_hbm_copy(pkg, torch_cuda, nbytes):
+    """The bandwidth-calibration copy (sdr_hbm_copy) copies every byte, ragged tails included, and
+    rejects misaligned sizes."""
+    torch = torch_cuda
+    g = torch.Generator(device="cuda").manual_seed(nbytes)
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+    dst = torch.zeros_like(src)
+    pkg.hbm_copy(dst, src)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src)
+    with pytest.raises(pkg.SdrError):
+        pkg.hbm_copy(dst[:nbytes - 8], src[:nbytes - 8])

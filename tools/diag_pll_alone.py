@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The PLL dispatch (stereo 19 kHz + RDS 114 kHz PLLs of 1024 channels, sdr_plls) alone on the chip
-versus inside the bench pipeline: fills one block's PLL inputs through the real stages, then times
-`plls()` back to back on one stream with nothing else running (the per-step cost without other
+versus inside the bench pipeline: runs the stages of each block on ONE stream and times
+the `plls()` dispatch between them, so nothing else runs beside it (the per-step cost without other
 kernels' HBM traffic), on all CUs and on a 64-CU masked stream as in the bench.
   python tools/diag_pll_alone.py [--iters 10]
 """
@@ -33,22 +33,25 @@ def main() -> None:
     created: list[int] = []
     _, s_pll, _ = bench.cu_masked_streams(torch, pkg, dev, "64", created)
     res = {"channels": nch, "chains": 2 * nch, "steps": n}
+    lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device=dev)
+    clean = torch.empty(nch, pipe.info.n_rds, dtype=torch.float32, device=dev)
     try:
-        for b in range(2):
-            pipe.frontend(iq[b], stream=s)
-            pipe.stereo_pre(stream=s)
-            pipe.rds_pre(stream=s)
-            pipe.plls(stream=s)
-        s.synchronize()
         for name, st in (("all_cus", s), ("cu_mask_64", s_pll)):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            pipe.plls(stream=st)
-            e0.record(st)
-            for _ in range(args.iters):
+            ev = []
+            for b in range(args.iters + 2):
+                # the stages before the PLLs on the same stream: nothing overlaps the PLL dispatch
+                pipe.frontend(iq[b % 2], stream=st)
+                pipe.stereo_pre(stream=st)
+                pipe.rds_pre(stream=st)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
                 pipe.plls(stream=st)
-            e1.record(st)
+                e1.record(st)
+                pipe.stereo_post(lr, stream=st)
+                pipe.rds_post(clean, bits=True, stream=st)
+                ev.append((e0, e1))
             st.synchronize()
-            ms = e0.elapsed_time(e1) / args.iters
+            ms = sum(a.elapsed_time(b) for a, b in ev[2:]) / args.iters
             res[name] = {"ms_per_block": round(ms, 4), "ns_per_step": round(ms * 1e6 / n, 2)}
     finally:
         pipe.close()
