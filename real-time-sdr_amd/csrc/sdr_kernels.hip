@@ -1408,7 +1408,13 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
                 for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
             }
             // refill (the last refills re-read the final chunk: harmless, keeps the loop branch-free)
+#if SDR_PLL_DIAG_L2
+            // diagnosis only (wrong results): every refill re-reads the first chunks (L2-resident),
+            // to measure what the HBM latency of the refills costs
+            load_chunk(xb[u], rb[u], u * C);
+#else
             load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
+#endif
 #if SDR_PLL_W01
             if (TAB) w01 = reinterpret_cast<const double2*>(wtab)[min(i0 + C, n - 2) >> 1];
 #endif
