@@ -7,7 +7,8 @@
 // IEC 62106 parity-check matrix and recognises offsets A, B, C, C', D, uint_copy (:313-337)
 // places the 16 data bits of A/B/C/D into a 64-bit group register, isSequenceABCD (:339-350)
 // tracks the last four offsets and parse (:172-199) prints PI, PTY and the Program Service name
-// of type-0 groups to stderr.
+// of type-0 groups to stderr. error_detection (:202-311, dead code in the reference) is the
+// alternative bit-serial synchroniser (f4).
 #include <cstdint>
 #include <cstdio>
 #include <deque>
@@ -102,6 +103,119 @@ void check_block(std::string& offset_type, std::vector<int>::iterator bitstream_
         return;
     }
     offset_type = "None";
+}
+
+// ---------------------------------------------------------------------------------------------
+// error_detection (src/rds_utilities.cpp:202-311): the reference's alternative,
+// bit-serial synchroniser. It is never called by the reference program (rds.cpp runs
+// start_frame_sync); it is served here so that the drop-in library covers rds_utilities.h:16
+// whole, with the reference's observable behaviour, quirks included:
+//   * unsynchronised, every bit prints the syndrome of the last 26 bits and the 64-bit history;
+//     two offset syndromes a whole number of blocks apart (in the offset order A B C D, C' in C's
+//     place) lock the block counter to the block after the second;
+//   * synchronised, every 26th bit checks one block (B / C' alternatives for block 2), counts bad
+//     blocks and, over each 50 blocks, drops sync when more than 40 were bad;
+//   * the group register passed to parse() holds only the current block's 16 data bits (it is
+//     cleared for every block), and parse() runs on the block that brings the good-block counter
+//     (+2 for a good block A, +1 for any other good block, never reset) to exactly 5.
+// The stderr text keeps the stream state the reference leaves (parse() switches std::cerr to hex).
+namespace {
+
+// x(z) z^10 mod g(z), g = z^10 + z^8 + z^7 + z^5 + z^4 + z^3 + 1 (0x5B9), over the low `nbits`
+// bits of x taken most significant first
+uint64_t crc10_syndrome(uint64_t x, int nbits) {
+    constexpr uint32_t kGen = 0x5B9;
+    uint32_t rem = 0;
+    for (int k = nbits + 9; k >= 0; k--) {
+        const uint32_t in = (k >= 10) ? static_cast<uint32_t>((x >> (k - 10)) & 1u) : 0u;
+        rem = (rem << 1) | in;
+        if (rem & 0x400u) rem ^= kGen;
+    }
+    return rem & 0x3FFu;
+}
+
+// offset words A, B, C, D, C' as received syndromes (unsynchronised search) and as checkword XOR
+// masks (synchronised check), and each offset's position in the block cycle
+constexpr uint64_t kSearchSyndrome[5] = {383, 14, 303, 663, 748};
+constexpr uint64_t kOffsetWord[5] = {252, 408, 360, 436, 848};
+constexpr int kCyclePos[5] = {0, 1, 2, 3, 2};
+
+}  // namespace
+
+void error_detection(uint64_t& reg, uint64_t& chars, uint64_t& output, bool& first_time, int& sync, int& prevsync,
+                     int& lastseen_offset, int& rds_bit_cont, int& lastseen_offset_cont, int& block_distance,
+                     int& block_number, int& block_bit_cont, int& blocks_cont, int& wrong_blocks_cont,
+                     int& group_assembly_started, int& group_good_blocks_cont, const std::vector<int>& decoded_bits) {
+    for (const int bit : decoded_bits) {
+        reg = (reg << 1) | static_cast<uint64_t>(static_cast<int64_t>(bit));
+        if (!sync) {
+            const uint64_t syn = crc10_syndrome(reg, 26);
+            std::cerr << "Reg Syndrome: " << syn << "    Reg: " << reg << std::endl;
+            int hit = -1;
+            for (int o = 0; o < 5 && hit < 0; o++)
+                if (syn == kSearchSyndrome[o]) hit = o;
+            if (hit >= 0) {
+                if (!prevsync) {
+                    lastseen_offset = hit;
+                    lastseen_offset_cont = rds_bit_cont;
+                    prevsync = 1;
+                } else {
+                    const int from = kCyclePos[lastseen_offset], to = kCyclePos[hit];
+                    block_distance = (from >= to) ? to + 4 - from : to - from;
+                    if (block_distance * 26 == rds_bit_cont - lastseen_offset_cont) {
+                        std::cerr << "Sync State Detected" << std::endl;
+                        wrong_blocks_cont = 0;
+                        blocks_cont = 0;
+                        block_bit_cont = 0;
+                        block_number = (hit + 1) & 3;
+                        group_assembly_started = 0;
+                        sync = 1;
+                    } else {
+                        prevsync = 0;
+                    }
+                }
+            }
+        } else if (block_bit_cont < 25) {
+            block_bit_cont++;
+        } else {
+            const uint64_t data = (reg >> 10) & 0xFFFF;
+            const uint64_t expect = crc10_syndrome(data, 16);
+            const uint64_t check = reg & 0x3FF;
+            bool good = (check ^ kOffsetWord[block_number]) == expect;
+            if (!good && block_number == 2) good = (check ^ kOffsetWord[4]) == expect;   // C'
+            if (!good) wrong_blocks_cont++;
+            uint64_t group = 0;   // cleared for every block (see above)
+            if (block_number == 0 && good) {
+                group_assembly_started = 1;
+                group_good_blocks_cont++;
+            }
+            if (group_assembly_started) {
+                if (good) {
+                    group = data << (48 - 16 * block_number);
+                    group_good_blocks_cont++;
+                } else {
+                    group_assembly_started = 0;
+                }
+                if (group_good_blocks_cont == 5) parse(group, chars, output, first_time);
+            }
+            block_bit_cont = 0;
+            block_number = (block_number + 1) & 3;
+            if (++blocks_cont == 50) {
+                if (wrong_blocks_cont > 40) {
+                    std::cerr << "Lost Sync (Got " << wrong_blocks_cont << " bad blocks on " << blocks_cont
+                              << " total)" << std::endl;
+                    sync = 0;
+                    prevsync = 0;
+                } else {
+                    std::cerr << "Still Sync-ed (Got " << wrong_blocks_cont << " bad blocks on " << blocks_cont
+                              << " total)" << std::endl;
+                }
+                blocks_cont = 0;
+                wrong_blocks_cont = 0;
+            }
+        }
+        rds_bit_cont++;
+    }
 }
 
 void start_frame_sync(unsigned int& idx, std::vector<int>& stream, std::vector<int>& sync_state_bits, uint64_t& reg,

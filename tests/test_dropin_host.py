@@ -33,7 +33,9 @@ EXPECTED = {
     "rds_utilities.h": ["cdr(int, std::vector<float> const&)",
                         "manchester_decode(std::vector<int>&, std::vector<int> const&, int&, int&, int&)",
                         "differential_decode(std::vector<int>&, std::vector<int> const&, int&, int&)",
-                        "parse(unsigned long const&, unsigned long&, unsigned long&, bool&)"],
+                        "parse(unsigned long const&, unsigned long&, unsigned long&, bool&)",
+                        "error_detection(unsigned long&, unsigned long&, unsigned long&, bool&, int&, int&, int&, "
+                        "int&, int&, int&, int&, int&, int&, int&, int&, int&, std::vector<int> const&)"],
     "stages": ["RF_frontend(args*)", "mono(args*)", "stereo(args*)", "rds(args*)"],
 }
 
@@ -89,6 +91,33 @@ def test_rds_frame_layer_matches_reference_text(golden_long, tmp_path):
         r = subprocess.run([str(exe)], input=feed, capture_output=True, text=True, check=True, timeout=60)
         assert r.stderr == fx["rds_text"], f"channel {ch}"
         assert "Program Service: MI355X" in r.stderr
+
+
+def test_error_detection_matches_reference(tmp_path):
+    """error_detection (reference rds_utilities.cpp:202-311, dead code there) served by
+    the drop-in frame layer reproduces the unmodified reference's stderr text byte for byte and its
+    final state, on the reference's decoded bits of the golden channels, the same with bit errors
+    and with a bit slip plus noise (sync lost and found again), and random bits (never syncs).
+    Fixtures: tests/golden/make_errdet.py (the reference's own rds_utilities.o)."""
+    import hashlib
+    import json
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = tmp_path / "errdet"
+    subprocess.run([gxx, "-O1", "-std=c++17", "-I", str(ROOT / "include" / "dropin"),
+                    str(ROOT / "tests" / "cpp" / "errdet_driver.cpp"),
+                    str(ROOT / "real-time-sdr_amd" / "host" / "rds_frame.cpp"), "-o", str(exe)], check=True)
+    fx = json.loads((ROOT / "tests" / "golden" / "golden_errdet.json").read_text())
+    seen = set()
+    for name, c in fx["cases"].items():
+        r = subprocess.run([str(exe)], input="\n".join(c["blocks"]) + "\n", capture_output=True, text=True,
+                           check=True, timeout=60)
+        assert r.stderr[:3000] == c["stderr_head"], name
+        assert hashlib.sha256(r.stderr.encode()).hexdigest() == c["stderr_sha256"], name
+        assert r.stdout.strip() == c["state"], name
+        seen |= {k for k in ("Sync State Detected", "Still Sync-ed", "Lost Sync", "PI: ") if k in r.stderr}
+    assert seen == {"Sync State Detected", "Still Sync-ed", "Lost Sync", "PI: "}   # every branch exercised
 
 
 def test_fm_batch_queue_protocol(tmp_path):
