@@ -171,7 +171,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // sched_barrier closes every sample so the scheduler keeps the sample-major order (ILP across the
 // R accumulators, each product next to its add) instead of hoisting products or serialising one
 // output's chain; the LDS chunk two chunks ahead is read at each chunk boundary.
-constexpr int FE_PF = 3;   // tap rows prefetched this many samples ahead (rotating SGPR ring)
+#ifndef SDR_FE_PF
+#define SDR_FE_PF 5
+#endif
+constexpr int FE_PF = SDR_FE_PF;   // tap rows prefetched this many samples ahead (rotating SGPR ring)
 
 // {h, h} * m with h one half (HI) of an SGPR pair: v_pk_mul_f32 with a scalar operand whose half
 // is broadcast to both lanes by op_sel / op_sel_hi (no VGPR copy of the tap)
@@ -532,7 +535,10 @@ __global__ __launch_bounds__(64) void k_frontend_mfma_q(
 // first fm_demod sample it writes (the discriminator's carry, demod.cpp:16); tiles advance by
 // 64*R-1. Boundary tiles (the first, which reads the previous block's tail, and the last, padded
 // with u8 128 = 0.0f) take a bytewise path.
-template <int R, int D, bool FAST>
+// PF: a persistent grid (SDR_FE_WG_PER_CU) that prefetches its next tile into registers during the
+// FIR; without it (the default, one tile per workgroup) the window registers die once the window is
+// in LDS, which leaves the FIR fewer VGPRs and the SIMD more waves.
+template <int R, int D, bool FAST, bool PF>
 __global__ __launch_bounds__(64) void k_frontend2(
     const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
     uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
@@ -623,7 +629,7 @@ __global__ __launch_bounds__(64) void k_frontend2(
             }
         }
         __syncthreads();
-        if (next < total) fetch(next);                // in flight during the FIR
+        if (PF && next < total) fetch(next);          // in flight during the FIR
         // ---- FIR: R outputs per thread, samples in descending order ----
         uint4 chunk[TCH];
         const uint4* tw = reinterpret_cast<const uint4*>(sw + 2 * t * R * D);
@@ -727,6 +733,7 @@ __global__ __launch_bounds__(64) void k_frontend2(
             const float* o = fm_other + (size_t)ch * fm_stride;
             for (int i = t; i < HIST; i += NTH) out[i - HIST] = o[block_if - HIST + i];
         }
+        if (!PF) break;                               // one tile per workgroup
         __syncthreads();                              // LDS is rewritten by the next tile
         tile = next;
     }
@@ -2509,10 +2516,11 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     // fe_grid == 0: one tile per workgroup (the hardware dispatcher balances the load when other
     // streams share the chip); otherwise a persistent grid that prefetches its next tile
     const dim3 g2(c->fe_grid > 0 ? std::min(total, c->fe_grid) : total);
-#define FE2(RR, DD, FF)                                                                                      \
-    hipLaunchKernelGGL((k_frontend2<RR, DD, FF>), g2, dim3(64), 0, S(stream), iq, iq_stride, tail_in, tail_out,  \
-                       prev_in, prev_out, c->rf_hs, in.block_iq, in.block_if, fm_p, fm_o, c->fm_stride, c->nch,   \
-                       tiles_ch, c->pad80)
+#define FE2P(RR, DD, FF, PP)                                                                                 \
+    hipLaunchKernelGGL((k_frontend2<RR, DD, FF, PP>), g2, dim3(64), 0, S(stream), iq, iq_stride, tail_in,        \
+                       tail_out, prev_in, prev_out, c->rf_hs, in.block_iq, in.block_if, fm_p, fm_o, c->fm_stride,  \
+                       c->nch, tiles_ch, c->pad80)
+#define FE2(RR, DD, FF) do { if (c->fe_grid > 0) FE2P(RR, DD, FF, true); else FE2P(RR, DD, FF, false); } while (0)
 #define FE2R(DD)                                                                                             \
     do {                                                                                                     \
         if (R == 8) { if (fast) FE2(8, DD, true); else FE2(8, DD, false); }                                  \
@@ -2561,6 +2569,7 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     }
 #undef FE2R
 #undef FE2
+#undef FE2P
     LAUNCH_CHECK();
     c->parity = p;
     c->block++;
