@@ -241,6 +241,9 @@ constexpr int FT_NB_DEFAULT = 32;
 #ifndef FT_RECOMB_F64
 #define FT_RECOMB_F64 0
 #endif
+#ifndef FT_DIAG
+#define FT_DIAG 0   // timing-only diagnosis of k_frontend_mfma (1: no compute, 2: no tap loads)
+#endif
 #ifndef FT_CT_UNROLL
 #define FT_CT_UNROLL 1
 #endif
@@ -415,8 +418,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
             }
         }
         // taps after the window: in flight together, the window (older) is waited for first
+#if FT_DIAG == 2
+        // timing-only diagnosis (wrong results): constant A fragments, no tap loads
+#pragma unroll
+        for (int f = 0; f < FT_AFRAGS; f++) A[f] = v4i{f, t, 1, 2};
+#else
 #pragma unroll
         for (int f = 0; f < FT_AFRAGS; f++) A[f] = afrag[f * 64 + t];
+#endif
         uint2* pi = reinterpret_cast<uint2*>(plane[0]);
         uint2* pq = reinterpret_cast<uint2*>(plane[1]);
 #pragma unroll
@@ -432,7 +441,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         }
     }
     __syncthreads();
+#if FT_DIAG == 1
+    // timing-only diagnosis (wrong results): staging and stores only, no MFMA / discriminator
+    {
+        const int lo = max(c0 + CARRY, 0), hi = min(c0 + CARRY + ADV, block_if);
+        const int8_t v0 = plane[0][t];
+        for (int c = lo + t; c < hi; c += 64) out[c] = (float)v0 + (float)A[0][0];
+    }
+#else
     ft_tile<D, NB, false>(plane[0], A, yscale, c0, ch, prev_in, prev_out, block_if, out);
+#endif
     if (j == 0) {
         const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
         uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
