@@ -253,7 +253,7 @@ constexpr int FT_NB_DEFAULT = 32;
 // and the persistent LDS-DMA kernel (raw image).
 template <int D, int NB, bool RAW>
 __device__ __forceinline__ void ft_tile(const int8_t* __restrict__ lds, const v4i (&A)[FT_AFRAGS], double yscale,
-                                        int c0, int ch, const float2* __restrict__ prev_in,
+                                        int c0, int ch, float2 prev_in_ch,
                                         float2* __restrict__ prev_out, int block_if, float* __restrict__ out) {
     constexpr int WIN = ft_win(D, NB), ADV = ft_adv(D, NB), CARRY = ft_carry(D);
     const float ys = (float)yscale;                   // 2^-(F+7): exact in f32
@@ -339,7 +339,7 @@ __device__ __forceinline__ void ft_tile(const int8_t* __restrict__ lds, const v4
             const int c = cb + r;
             float qI = aI[r], qQ = aQ[r];
             if (c == 0) {
-                const float2 pv = prev_in[ch];
+                const float2 pv = prev_in_ch;
                 qI = pv.x;
                 qQ = pv.y;
             }
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         for (int c = lo + t; c < hi; c += 64) out[c] = (float)v0 + (float)A[0][0];
     }
 #else
-    ft_tile<D, NB, false>(plane[0], A, yscale, c0, ch, prev_in, prev_out, block_if, out);
+    ft_tile<D, NB, false>(plane[0], A, yscale, c0, ch, prev_in[ch], prev_out, block_if, out);
 #endif
     if (j == 0) {
         const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(64) void k_frontend_mfma_q(
         __builtin_amdgcn_s_barrier();
         const int ch = cur / tiles_ch, j = cur - ch * tiles_ch;
         float* out = fm + (size_t)ch * fm_stride;
-        ft_tile<D, NB, true>(lds + b * BUFB, A, yscale, j * ADV - CARRY, ch, prev_in, prev_out, block_if, out);
+        ft_tile<D, NB, true>(lds + b * BUFB, A, yscale, j * ADV - CARRY, ch, prev_in[ch], prev_out, block_if, out);
         if (j == 0) {
             const uint8_t* src = iq + (size_t)ch * iq_stride;
             const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
@@ -543,6 +543,102 @@ __global__ __launch_bounds__(64) void k_frontend_mfma_q(
         cur = nxt;
         nxt += G;
         b ^= 1;
+    }
+}
+
+// Persistent MFMA front end with register prefetch (SDR_FE_MFMA_WPE = waves per SIMD): a grid of
+// 4*WPE one-wave workgroups per CU walks tiles round-robin (tile = blockIdx.x + i*gridDim.x). Each
+// wave loads the taps' A fragments once (16 KiB per wave instead of per tile) and keeps the NEXT
+// tile's window in flight in registers (the same 16-byte I/Q group loads as k_frontend_mfma) while
+// the current tile computes out of its single LDS image, so one image per wave lets more waves
+// fit than the two-buffer LDS-DMA kernel. 16-byte aligned rows only (the launcher checks).
+template <int D, int NB, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_frontend_mfma_p(
+    const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
+    uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
+    const v4i* __restrict__ afrag, double yscale, int block_iq, int block_if,
+    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int tiles_ch, int total,
+    const uint32_t* __restrict__ pad) {
+    static_assert(15 * D + 101 <= 256 && NB % 8 == 0, "tile geometry");
+    constexpr int HP = 100, WIN = ft_win(D, NB), G = WIN / 8;
+    constexpr int ADV = ft_adv(D, NB), CARRY = ft_carry(D);
+    constexpr int GPL = (G + 63) / 64;                // 16-byte groups per lane
+    __shared__ __attribute__((aligned(16))) int8_t plane[2][WIN];
+    const int t = threadIdx.x;
+    int cur = blockIdx.x;
+    if (cur >= total) return;
+    v4i A[FT_AFRAGS];
+#pragma unroll
+    for (int f = 0; f < FT_AFRAGS; f++) A[f] = afrag[f * 64 + t];
+    uint4 st[GPL];
+    // window of tile tl -> st (lane t holds groups t, t+64, ...): interior windows as one dwordx4
+    // per group, boundary windows (previous block's tail, padding past the block) per 8 bytes
+    auto fetch = [&](int tl) {
+        const int ch = tl / tiles_ch, j = tl - ch * tiles_ch;
+        const int m0 = (j * ADV - CARRY) * D - HP;    // = 0 mod 8
+        const uint8_t* src = iq + (size_t)ch * iq_stride;
+        if (m0 >= 0 && m0 + WIN <= block_iq) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4* gw = reinterpret_cast<const u32x4*>(src + 2 * m0);
+#pragma unroll
+            for (int k = 0; k < GPL; k++) {
+                const int i = t + 64 * k;
+                const u32x4 v = (k < GPL - 1 || i < G) ? __builtin_nontemporal_load(gw + i) : u32x4{0u, 0u, 0u, 0u};
+                st[k] = uint4{v.x, v.y, v.z, v.w};
+            }
+        } else {
+            const uint2* g2 = reinterpret_cast<const uint2*>(src);
+            const uint2* t2 = reinterpret_cast<const uint2*>(tail_in + (size_t)ch * 2 * HP);
+            const uint2* p2 = reinterpret_cast<const uint2*>(pad);
+#pragma unroll
+            for (int k = 0; k < GPL; k++) {
+                uint2 h[2];
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    const int mm = m0 + 8 * (t + 64 * k) + 4 * hh;
+                    const uint2* pa = mm >= 0 ? (mm < block_iq ? g2 + (mm >> 2) : p2)
+                                              : (mm >= -HP ? t2 + ((HP + mm) >> 2) : p2);
+                    h[hh] = *pa;
+                }
+                st[k] = uint4{h[0].x, h[0].y, h[1].x, h[1].y};
+            }
+        }
+    };
+    fetch(cur);
+    while (true) {
+        {   // st -> planar signed I and Q rows
+            uint2* pi = reinterpret_cast<uint2*>(plane[0]);
+            uint2* pq = reinterpret_cast<uint2*>(plane[1]);
+#pragma unroll
+            for (int k = 0; k < GPL; k++) {
+                const int i = t + 64 * k;
+                if (k < GPL - 1 || i < G) {
+                    const uint4 v = st[k];
+                    pi[i] = uint2{__builtin_amdgcn_perm(v.y, v.x, 0x06040200u) ^ 0x80808080u,
+                                  __builtin_amdgcn_perm(v.w, v.z, 0x06040200u) ^ 0x80808080u};
+                    pq[i] = uint2{__builtin_amdgcn_perm(v.y, v.x, 0x07050301u) ^ 0x80808080u,
+                                  __builtin_amdgcn_perm(v.w, v.z, 0x07050301u) ^ 0x80808080u};
+                }
+            }
+        }
+        const int ch = cur / tiles_ch, j = cur - ch * tiles_ch;
+        const float2 prev = prev_in[ch];              // before the prefetch: its wait must not cover it
+        __syncthreads();
+        const int nxt = cur + (int)gridDim.x;
+        if (nxt < total) fetch(nxt);                  // in flight during this tile's MFMA and discriminator
+        float* out = fm + (size_t)ch * fm_stride;
+        ft_tile<D, NB, false>(plane[0], A, yscale, j * ADV - CARRY, ch, prev, prev_out, block_if, out);
+        if (j == 0) {
+            const uint8_t* src = iq + (size_t)ch * iq_stride;
+            const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
+            uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
+            for (int i = t; i < HP; i += 64) tout[i] = last[i];
+            const float* o = fm_other + (size_t)ch * fm_stride;
+            for (int i = t; i < HIST; i += 64) out[i - HIST] = o[block_if - HIST + i];
+        }
+        if (nxt >= total) break;
+        cur = nxt;
+        __syncthreads();                              // the LDS image is rewritten next
     }
 }
 
@@ -2098,6 +2194,8 @@ struct sdr_ctx {
     double fe_yscale = 0.0;                             // 2^-(F+7): fixed-point taps, x = (u-128)/128
     bool fe_mfma = false;                               // fast mode runs k_frontend_mfma
     int fe_nb = FT_NB_DEFAULT;                          // MFMA front end: 16-output blocks per tile
+    int fe_wpe = 0;                                     // > 0: persistent register-prefetch MFMA front end
+    int cus = 0;                                        // compute units of the device
     int parity = 1;                                     // parity of the current block
     long long block = -1;                               // index of the current block
     long long stereo_done = -1, rds_dsp_done = -1, rds_bits_done = -1, mono_done = -1;
@@ -2356,6 +2454,11 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
         // 2.5x faster while the other streams' kernels share the chip (the dispatcher balances).
         int cus = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        c->cus = cus;
+        if (const char* e = std::getenv("SDR_FE_MFMA_WPE")) {    // tuning knob: persistent MFMA, waves per SIMD
+            const int k = std::atoi(e);
+            if (k >= 2 && k <= 4) c->fe_wpe = k;
+        }
         if (const char* e = std::getenv("SDR_FE_WG_PER_CU")) {   // tuning knob: persistent grid, k per CU
             const int k = std::atoi(e);
             if (k >= 0 && cus > 0) c->fe_grid = k * cus;
@@ -2548,10 +2651,18 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
         const v4i* af = static_cast<const v4i*>(c->fe_afrag);
         // 16-byte I/Q group loads need 16-byte aligned rows (e.g. a row stride of 147008 for mode 0)
         const bool x4 = (iq_stride % 16 == 0) && (reinterpret_cast<uintptr_t>(iq) % 16 == 0);
+#define FEMP(DD, NB, W)                                                                                      \
+    hipLaunchKernelGGL((k_frontend_mfma_p<DD, (NB == 16 ? 16 : 32), W>), gp, dim3(64), 0, S(stream), iq, iq_stride, \
+                       tail_in, tail_out, prev_in, prev_out, af, c->fe_yscale, in.block_iq, in.block_if, fm_p,     \
+                       fm_o, c->fm_stride, tc, tc * c->nch, c->pad80)
 #define FEM(DD, XX, NB)                                                                                      \
     do {                                                                                                     \
         const int tc = cdiv(in.block_if, ft_adv(DD, NB));                                                    \
-        if (XX && c->fe_grid > 0) {                                                                          \
+        if (XX && c->fe_wpe > 0 && (NB == 16 || NB == 32)) {                                                 \
+            const int g = c->fe_grid > 0 ? c->fe_grid : 4 * c->fe_wpe * c->cus;                              \
+            const dim3 gp(std::min(tc * c->nch, g));                                                         \
+            if (c->fe_wpe == 2) FEMP(DD, NB, 2); else if (c->fe_wpe == 4) FEMP(DD, NB, 4); else FEMP(DD, NB, 3); \
+        } else if (XX && c->fe_grid > 0) {                                                                   \
             hipLaunchKernelGGL((k_frontend_mfma_q<DD, NB>), dim3(std::min(tc * c->nch, c->fe_grid)), dim3(64), \
                                0, S(stream), iq, iq_stride, tail_in, tail_out, prev_in, prev_out, af,        \
                                c->fe_yscale, in.block_iq, in.block_if, fm_p, fm_o, c->fm_stride, tc,          \
@@ -2571,6 +2682,7 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
         else { if (x4) FEMN(3, true); else FEMN(3, false); }
 #undef FEMN
 #undef FEM
+#undef FEMP
     } else if (c->ntaps == 101 && in.rf_decim == 10) {
         FE2R(10);
     } else if (c->ntaps == 101 && in.rf_decim == 4) {
