@@ -362,6 +362,97 @@ __device__ __forceinline__ void ft_tile(const int8_t* __restrict__ lds, const v4
     }
 }
 
+// The same wave tile with I and Q of one block in ONE lane (FT_IQLANE, NB a multiple of 16): a
+// C tile is 16 blocks, columns = blocks, and the I and Q planes are two MFMA groups with the same A
+// fragments, so lane t holds rows 4g..4g+3 of block 16*ct + (t & 15) for both components. The
+// discriminator then needs no DPP exchange or component selects, each lane finishes 4 outputs, and
+// one pair of shuffles per C tile brings the previous row (lane t-16, or row 15 of the previous block).
+template <int D, int NB>
+__device__ __forceinline__ void ft_tile_iq(const int8_t* __restrict__ lds, const v4i (&A)[FT_AFRAGS], double yscale,
+                                           int c0, int ch, float2 prev_in_ch, float2* __restrict__ prev_out,
+                                           int block_if, float* __restrict__ out) {
+    static_assert(NB % 16 == 0, "whole 16-block C tiles");
+    constexpr int WIN = ft_win(D, NB), ADV = ft_adv(D, NB), CARRY = ft_carry(D);
+    const float ys = (float)yscale;
+    const int t = threadIdx.x;
+    const int n = t & 15, g = t >> 4;
+    const int lo = max(c0 + CARRY, 0), hi = min(c0 + CARRY + ADV, block_if);
+    // row 4g - 1 of this block (lane t - 16) or row 15 of the previous block (lane 48 + n - 1)
+    const int src_lane = g > 0 ? t - 16 : (n > 0 ? t + 47 : t);
+    float carry_i = 0.0f, carry_q = 0.0f;             // row 15 of the previous C tile's last block
+#pragma unroll FT_CT_UNROLL
+    for (int ct = 0; ct < NB / 16; ct++) {
+        const int bb = 16 * ct + n;
+        v4i aI[FT_ND], aQ[FT_ND];
+#pragma unroll
+        for (int p = 0; p < FT_ND; p++) { aI[p] = v4i{0, 0, 0, 0}; aQ[p] = v4i{0, 0, 0, 0}; }
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+            const int off = 16 * D * bb + 64 * kk + 16 * g;
+            const v4i BI = *reinterpret_cast<const v4i*>(lds + off);
+            const v4i BQ = *reinterpret_cast<const v4i*>(lds + WIN + off);
+#pragma unroll
+            for (int p = 0; p < FT_ND; p++) {
+                aI[p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[FT_ND * kk + p], BI, aI[p], 0, 0, 0);
+                aQ[p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[FT_ND * kk + p], BQ, aQ[p], 0, 0, 0);
+            }
+        }
+        static_assert(FT_ND == 4, "pairwise recombination assumes 4 digit planes");
+        float yI[4], yQ[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            // digits pair up exactly in int32, then one fma in f32 (as ft_tile)
+            const int hI = (aI[0][r] << 8) + aI[1][r], lI = (aI[2][r] << 8) + aI[3][r];
+            const int hQ = (aQ[0][r] << 8) + aQ[1][r], lQ = (aQ[2][r] << 8) + aQ[3][r];
+            yI[r] = __builtin_fmaf((float)hI, ys * 65536.0f, (float)lI * ys);
+            yQ[r] = __builtin_fmaf((float)hQ, ys * 65536.0f, (float)lQ * ys);
+        }
+        const float sI = __shfl(yI[3], src_lane), sQ = __shfl(yQ[3], src_lane);
+        const bool first = (t == 0);
+        const float pI = first ? carry_i : sI, pQ = first ? carry_q : sQ;
+        carry_i = __shfl(yI[3], 63);
+        carry_q = __shfl(yQ[3], 63);
+        const int cb = c0 + 16 * bb + 4 * g;          // output index of this lane's first row
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int c = cb + r;
+            float qI = r == 0 ? pI : yI[r > 0 ? r - 1 : 0], qQ = r == 0 ? pQ : yQ[r > 0 ? r - 1 : 0];
+            if (c == 0) {
+                qI = prev_in_ch.x;
+                qQ = prev_in_ch.y;
+            }
+            const float cI = yI[r], cQ = yQ[r];
+            // demod.cpp:8-19 (fast mode: f32 denominator and a v_rcp_f32 quotient, as ft_tile)
+            const float num = cI * (cQ - qQ) - cQ * (cI - qI);
+            const float den = cI * cI + cQ * cQ;
+            const float q = num * __builtin_amdgcn_rcpf(den);
+            v[r] = ((cI == 0.0f) & (cQ == 0.0f)) ? 0.0f : q;
+            if (c == block_if - 1) prev_out[ch] = make_float2(cI, cQ);
+        }
+        if (cb >= lo && cb + 3 < hi && ((cb & 1) == 0)) {
+            *reinterpret_cast<float2*>(out + cb) = make_float2(v[0], v[1]);
+            *reinterpret_cast<float2*>(out + cb + 2) = make_float2(v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if (cb + r >= lo && cb + r < hi) out[cb + r] = v[r];
+        }
+    }
+}
+#ifndef FT_IQLANE
+#define FT_IQLANE 1   // I and Q of a block in one lane (ft_tile_iq) when NB is a multiple of 16
+#endif
+template <int D, int NB>
+__device__ __forceinline__ void ft_tile_planar(const int8_t* __restrict__ lds, const v4i (&A)[FT_AFRAGS], double yscale,
+                                               int c0, int ch, float2 prev_in_ch, float2* __restrict__ prev_out,
+                                               int block_if, float* __restrict__ out) {
+    if constexpr (FT_IQLANE && NB % 16 == 0)
+        ft_tile_iq<D, NB>(lds, A, yscale, c0, ch, prev_in_ch, prev_out, block_if, out);
+    else
+        ft_tile<D, NB, false>(lds, A, yscale, c0, ch, prev_in_ch, prev_out, block_if, out);
+}
+
 template <int D, bool X4, int NB>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_frontend_mfma(
     const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
@@ -449,7 +540,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         for (int c = lo + t; c < hi; c += 64) out[c] = (float)v0 + (float)A[0][0];
     }
 #else
-    ft_tile<D, NB, false>(plane[0], A, yscale, c0, ch, prev_in[ch], prev_out, block_if, out);
+    ft_tile_planar<D, NB>(plane[0], A, yscale, c0, ch, prev_in[ch], prev_out, block_if, out);
 #endif
     if (j == 0) {
         const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
@@ -627,7 +718,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
         const int nxt = cur + (int)gridDim.x;
         if (nxt < total) fetch(nxt);                  // in flight during this tile's MFMA and discriminator
         float* out = fm + (size_t)ch * fm_stride;
-        ft_tile<D, NB, false>(plane[0], A, yscale, j * ADV - CARRY, ch, prev, prev_out, block_if, out);
+        ft_tile_planar<D, NB>(plane[0], A, yscale, j * ADV - CARRY, ch, prev, prev_out, block_if, out);
         if (j == 0) {
             const uint8_t* src = iq + (size_t)ch * iq_stride;
             const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
