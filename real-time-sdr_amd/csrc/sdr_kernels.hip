@@ -174,6 +174,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #ifndef SDR_FE_PF
 #define SDR_FE_PF 5
 #endif
+#ifndef SDR_FE_CVT_MID
+#define SDR_FE_CVT_MID 0   // 1: conversion between the products (more hazard wait states: not adopted)
+#endif
 constexpr int FE_PF = SDR_FE_PF;   // tap rows prefetched this many samples ahead (rotating SGPR ring)
 
 // {h, h} * m with h one half (HI) of an SGPR pair: v_pk_mul_f32 with a scalar operand whose half
@@ -892,8 +895,15 @@ __global__ __launch_bounds__(64) void k_frontend2(
                 for (int r = 0; r < R; r++) {
                     const int k = r * D + HP - S;
                     if (k >= 0 && k < NT) prod[r] = fe_mul_v(ring[slot][r >> 1], r & 1, m);
+#if SDR_FE_CVT_MID
+                    // the next sample's conversion between the products (an inline-asm result
+                    // read right after it costs a wait state; here nothing reads it until S - 1)
+                    if (r == R / 2 - 1 && S > 0) m_next = sample(S - 1);
+#endif
                 }
+#if !SDR_FE_CVT_MID
                 if (S > 0) m_next = sample(S - 1);
+#endif
 #pragma unroll
                 for (int r = 0; r < R; r++) {
                     const int k = r * D + HP - S;
@@ -1382,6 +1392,9 @@ struct PllProof {
     uint32_t tie = ~0u;
     float tmax = 0.0f;
 };
+#ifndef SDR_PLL_LF_SCALAR
+#define SDR_PLL_LF_SCALAR 1   // the plain f32 loop filter (no inline asm): +1.2 %, profiles/r02/ab_pll_lf.txt
+#endif
 #ifndef SDR_PLL_EDHI
 #define SDR_PLL_EDHI 0
 #endif
@@ -1466,10 +1479,21 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
     }
     // pll.cpp:41-42: integ += Ki e; phaseEst = (phaseEst + Kp e) + integ, with the two products
     // and the two first sums as one v_pk_mul_f32 + one v_pk_add_f32 (the same f32 roundings)
+#if SDR_PLL_LF_SCALAR
+    // scalar f32: 5 VALU, and no hazard wait states after packed-f32 results
+    {
+        float ki_e = Ki * e;
+        if (SDR_PLL_LF_SCALAR == 2) asm("" : "+v"(ki_e));      // keeps the SLP vectoriser from packing
+        const float integ = r.ip.x + ki_e;
+        r.ip.y = (r.ip.y + Kp * e) + integ;
+        r.ip.x = integ;
+    }
+#else
     r.ip = r.ip + f32x2{Ki, Kp} * f32x2{e, e};
     float ph = r.ip.y;                                        // in place (else a pk_add + move)
     asm("v_add_f32 %0, %0, %1" : "+v"(ph) : "v"(r.ip.x));
     r.ip.y = ph;
+#endif
     float t;
     if (TAB) {                                                // wt = w * trigOffset, tabulated
         t = (float)(wt + (double)r.ip.y);                     // pll.cpp:47
