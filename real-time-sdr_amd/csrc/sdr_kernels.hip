@@ -1392,6 +1392,12 @@ struct PllProof {
     uint32_t tie = ~0u;
     float tmax = 0.0f;
 };
+#ifndef SDR_PLL_HI_FIRST
+#define SDR_PLL_HI_FIRST 1
+#endif
+#ifndef SDR_PLL_PREWAIT
+#define SDR_PLL_PREWAIT 0
+#endif
 #ifndef SDR_PLL_LF_SCALAR
 #define SDR_PLL_LF_SCALAR 1   // the plain f32 loop filter (no inline asm): +1.2 %, profiles/r02/ab_pll_lf.txt
 #endif
@@ -1464,7 +1470,14 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
     const float lo = (float)pllm::fma_(Y, rx, base - pllm::EPS_ABS_E2), hi = (float)ed;
 #else
     const double ed = pllm::fma_(Y, rx, base);
+#if SDR_PLL_HI_FIRST
+    // hi (the value used) first: the loop filter's packed product can issue while lo, the range
+    // and the split test fill its hazard wait states
+    const float hi = (float)(ed + pllm::EPS_ABS_E2);
+    const float lo = (float)(ed - pllm::EPS_ABS_E2);
+#else
     const float lo = (float)(ed - pllm::EPS_ABS_E2), hi = (float)(ed + pllm::EPS_ABS_E2);
+#endif
 #endif
     float e = hi;                                             // = RN32(ed) whenever lo == hi
     if (CHECKED) {
@@ -1599,6 +1612,14 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
     if (nmain > 0) {
 #pragma unroll
         for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
+#if SDR_PLL_PREWAIT
+        // the first buffers land before the loop (one memory latency per block). Otherwise the
+        // compiler's wait counts at the loop header merge these loads' positions with the back
+        // edge's and the steady-state loop waits for loads and stores it does not need: vmcnt(4)
+        // before every refill (the previous chunk's refill) and vmcnt(12) inside every chunk (the
+        // stores just issued), exposing a memory latency per chunk.
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt and lgkmcnt unconstrained (gfx9)
+#endif
     }
 #if SDR_PLL_W01
     double2 w01 = TAB ? reinterpret_cast<const double2*>(wtab)[0] : double2{0.0, 0.0};
