@@ -266,6 +266,7 @@ class GpuStepper:
         else:
             pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
         achieved = fe_bytes / fe_avg_s / 1e9
+        redo = self._pll_redo()
         kname = ("k_frontend_mfma" if self.fast else "k_frontend2") + " (u8 I/Q -> 101-tap FIR /10 on I,Q -> FM discriminator)"
         return {
             "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -278,8 +279,22 @@ class GpuStepper:
                     "bound": "serial recurrence: block_if dependent steps per chain, one lane per chain "
                              "(per-wave VALU issue, DESIGN.md 4a)",
                     "avg_launch_ms": round(pll_ms, 4), "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
-                    "share_of_step": round(pll_ms / (elapsed / steps * 1e3), 4)},
+                    "share_of_step": round(pll_ms / (elapsed / steps * 1e3), 4),
+                    **({"chunk_redo": redo} if redo else {})},
         }
+
+    def _pll_redo(self) -> dict | None:
+        """Diagnosis builds (-DSDR_PLL_COUNT=1) only: fraction of the PLL's 16-step chunks whose proof
+        failed (per lane) and that a wave redid with the checked path, over warm-up and timed blocks."""
+        import ctypes as C
+        f = getattr(self.pkg.lib(), "sdr_diag_pll_counts", None)
+        if f is None:
+            return None
+        c = (C.c_ulonglong * 4)()
+        if f(c, 0) != 0 or c[0] == 0:
+            return None
+        return {"lane_chunks": c[0], "lane_fail_frac": c[1] / c[0], "wave_chunks": c[2],
+                "wave_redo_frac": c[3] / max(c[2], 1)}
 
     def isolated_frontend(self) -> dict:
         """Outside the timed region: the front-end kernel of both numerics modes alone on the GPU

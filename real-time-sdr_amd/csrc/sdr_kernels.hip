@@ -1408,6 +1408,24 @@ struct PllProof {
 constexpr double PLL_EMAX = SDR_PLL_EDHI ? pllm::PI - 0x1p-30 - 0x1p-42 : pllm::PI - 0x1p-30;
 constexpr double PLL_TAB_WT_MAX = 0x1.6p29;   // |w * trigOffset| bound of the table path (above)
 
+#ifndef SDR_PLL_COUNT
+#define SDR_PLL_COUNT 0   // diagnosis build: count the fast chunks and the redone ones (sdr_diag_pll_counts)
+#endif
+#if SDR_PLL_COUNT
+// [lane-chunks, lane-chunks that failed their proof, wave-chunks, wave-chunks redone]
+__device__ unsigned long long g_pll_counts[4];
+__device__ __forceinline__ void pll_count_chunk(bool ok) {
+    const unsigned long long exec = __builtin_amdgcn_read_exec();
+    const unsigned long long bad = __ballot(!ok) & exec;
+    if ((int)__lane_id() == __ffsll((long long)exec) - 1) {
+        atomicAdd(&g_pll_counts[0], (unsigned long long)__popcll(exec));
+        atomicAdd(&g_pll_counts[1], (unsigned long long)__popcll(bad));
+        atomicAdd(&g_pll_counts[2], 1ull);
+        atomicAdd(&g_pll_counts[3], bad ? 1ull : 0ull);
+    }
+}
+#endif
+
 // TAB: the trigArg offsets come from a table whose range the kernel checked once (pll_run)
 template <bool TAB>
 __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
@@ -1650,7 +1668,11 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
 #pragma unroll
             for (int j = 0; j < C; j++)
                 pll_step<false, TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
-            if (!pll_chunk_ok<TAB>(pf, r, w, C)) {
+            const bool chunk_ok = pll_chunk_ok<TAB>(pf, r, w, C);
+#if SDR_PLL_COUNT
+            pll_count_chunk(chunk_ok);
+#endif
+            if (!chunk_ok) {
                 r = snap;
 #pragma unroll
                 for (int j = 0; j < C; j++)
@@ -2570,6 +2592,23 @@ int sdr_hbm_copy(void* dst, const void* src, size_t bytes, void* stream) {
                        static_cast<const u32x4*>(src), n);
     HIP_TRY(hipGetLastError());
     return SDR_OK;
+}
+
+// Diagnosis builds only (-DSDR_PLL_COUNT=1): the PLL chunk counters [lane-chunks, failed lane-chunks,
+// wave-chunks, redone wave-chunks], optionally reset; -1 in product builds. Not part of sdr_amd.h.
+extern "C" int sdr_diag_pll_counts(unsigned long long* out, int reset) {
+#if SDR_PLL_COUNT
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pll_counts), sizeof(unsigned long long) * 4));
+    if (reset) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pll_counts), z, sizeof z));
+    }
+    return SDR_OK;
+#else
+    (void)out;
+    (void)reset;
+    return -1;
+#endif
 }
 
 int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int flags) {
