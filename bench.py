@@ -469,7 +469,8 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
                 res["roofline"]["copy_GBps"] = iso["hbm_copy"]["achieved"]
                 res["roofline"]["frac_of_copy"] = round(res["roofline"]["achieved"] / iso["hbm_copy"]["achieved"], 4)
                 res["roofline_fast"] = iso.get("fast")
-            res["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_leg(args, st.captured())
+            res["cpu_baseline"] = (None if args.no_cpu_baseline
+                                   else cpu_baseline_leg(args, st.captured(), timing=(world == 1)))
             res["verified"] = (res["cpu_baseline"] or {}).get("verified", {}).get("ok")
         return res
     finally:
@@ -542,7 +543,7 @@ def _check_channel(job):
     return j, bad[:4]
 
 
-def cpu_baseline_leg(args, cap: dict | None) -> dict:
+def cpu_baseline_leg(args, cap: dict | None, timing: bool = True) -> dict:
     """Rank 0 only, outside the timed region: (1) the reference's own program (oracle/_ref/project,
     built from the unmodified sources) in its 3-thread topology on one channel; (2) the same
     program on distinct channels concurrently over the host's CPU share (floor(cores/3) processes);
@@ -552,7 +553,12 @@ def cpu_baseline_leg(args, cap: dict | None) -> dict:
     exe = ROOT / "oracle" / "_ref" / "project"
     cores = _cpu_share()
     res: dict = {"host_cpu": _cpu_model(), "nproc": os.cpu_count(), "cpu_share": cores}
-    if exe.exists():
+    if not timing:
+        # N > 1: the CPU legs are timed at N = 1 only (BASELINE's CPU comparison is per node, and the
+        # other ranks have finished); the captured outputs are still checked below
+        res.update({"value": None, "unit": "MS/s", "cores": 0, "kind": "reference",
+                    "sample": "not timed at N > 1 (see the N = 1 line)"})
+    elif exe.exists():
         nblk = 32
         blob = _blob(0, nblk)
         reps = 150  # 4800 blocks = 353 M I/Q samples (~10 s at the reference's ~37 MS/s)

@@ -236,3 +236,14 @@ def test_bench_gpus_flag_fails_without_gpus():
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0
     assert "GPU(s) visible" in r.stderr
+
+
+def test_cpu_baseline_untimed_above_one_gpu():
+    """At N > 1 the CPU baseline legs are not re-timed (they are quoted on the N = 1 line); the
+    rank-0 line still carries the object, with value None and the reason."""
+    import argparse
+    import sys
+    sys.path.insert(0, str(ROOT))
+    import bench
+    res = bench.cpu_baseline_leg(argparse.Namespace(), None, timing=False)
+    assert res["value"] is None and "N > 1" in res["sample"] and "verified" not in res
