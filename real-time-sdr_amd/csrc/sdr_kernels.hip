@@ -189,9 +189,18 @@ __device__ __forceinline__ f32x2 fe_mul_v(double hpair, int hi, f32x2 m) {
 }
 // (I, Q) of one sample, sign-extended from the bytes of a dword that holds two samples
 // (u8 ^ 0x80 == u8 - 128 as int8), converted in program order (volatile asm)
+#ifndef SDR_FE_CVT_C
+#define SDR_FE_CVT_C 0
+#endif
 template <int HALF>
 __device__ __forceinline__ f32x2 fe_cvt_v(uint32_t w) {
     f32x2 r;
+#if SDR_FE_CVT_C
+    // plain C++ (the SDWA peephole forms the same sext-byte conversions): no inline-asm hazard
+    r.x = (float)(int)(int8_t)(uint8_t)(w >> (16 * HALF));
+    r.y = (float)(int)(int8_t)(uint8_t)(w >> (16 * HALF + 8));
+    return r;
+#endif
     if (HALF) {
         asm volatile("v_cvt_f32_i32_sdwa %0, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2\n\t"
                      "v_cvt_f32_i32_sdwa %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3"
@@ -203,10 +212,17 @@ __device__ __forceinline__ f32x2 fe_cvt_v(uint32_t w) {
     }
     return r;
 }
+#ifndef SDR_FE_ADD_C
+#define SDR_FE_ADD_C 0
+#endif
 __device__ __forceinline__ f32x2 fe_add_v(f32x2 a, f32x2 b) {
+#if SDR_FE_ADD_C
+    return a + b;   // v_pk_add_f32, ordered by its operands (no inline-asm hazard wait after the products)
+#else
     f32x2 r;
     asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
+#endif
 }
 __device__ __forceinline__ f32x2 fe_fma(double hpair, int hi, f32x2 m, f32x2 acc) {
     f32x2 r;
