@@ -12,8 +12,9 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-g
             -mllvm -pragma-unroll-threshold=1000000 \
             -Wall -Iinclude
 LIB      := $(PKG)/libsdr_amd.so
-SRCS     := $(PKG)/csrc/sdr_kernels.hip $(PKG)/csrc/sdr_taps.cpp
-HDRS     := include/sdr_amd.h $(PKG)/csrc/pll_math.h
+SRCS     := $(PKG)/csrc/sdr_kernels.hip $(PKG)/csrc/sdr_frontend.hip $(PKG)/csrc/sdr_pll.hip $(PKG)/csrc/sdr_taps.cpp
+OBJS     := $(patsubst $(PKG)/csrc/%,build/%.o,$(SRCS))
+HDRS     := include/sdr_amd.h $(PKG)/csrc/pll_math.h $(PKG)/csrc/sdr_internal.h
 
 # host C++ (no device code): compiled by the system g++ against the HIP runtime headers
 HOSTFLAGS := -O2 -std=c++17 -fPIC -Wall -Wextra -pthread -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include \
@@ -30,8 +31,13 @@ all: lib host oracle
 lib: $(LIB)
 host: $(HOSTLIB) $(CLI) $(MULTI)
 
-$(LIB): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,libsdr_amd.so -o $@ $(SRCS)
+# one object per translation unit (compiled in parallel), linked into the shared library
+build/%.o: $(PKG)/csrc/% $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -fPIC -shared -Wl,-soname,libsdr_amd.so -o $@ $(OBJS)
 
 $(HOSTLIB): $(HOSTSRCS) $(HOSTHDRS) $(LIB)
 	$(CXX) $(HOSTFLAGS) -shared -o $@ $(HOSTSRCS) -L$(PKG) -lsdr_amd -L$(ROCM)/lib -lamdhip64 \
@@ -51,4 +57,5 @@ oracle: host
 
 clean:
 	rm -f $(LIB) $(HOSTLIB) $(CLI) $(MULTI)
+	rm -rf build
 	$(MAKE) -C oracle clean

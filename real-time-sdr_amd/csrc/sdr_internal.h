@@ -1,0 +1,189 @@
+// sdr_internal.h -- declarations shared by the translation units of libsdr_amd.so (not installed).
+//
+//   sdr_frontend.hip   u8 I/Q -> 101-tap FIR /D on I and Q -> discriminator   rffrontend.cpp:58-71
+//   sdr_pll.hip        PLL / NCO recurrences, persistent PLL hand-offs        pll.cpp:4-61
+//   sdr_kernels.hip    IF FIRs, resamplers, mixers, RDS bits, context and the C ABI
+//
+// Layout: channel-major [nch][len]. Every f32 stream that a later FIR/resampler reads with
+// look-back is kept "extended": [2 parities][nch][HIST + len], the first HIST samples being the
+// previous block's last HIST samples, so a kernel reads x[-HIST..len) with no branch; the
+// producer of block b copies the history from the parity of block b-1.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "sdr_amd.h"
+
+#define SDRK_HIDDEN __attribute__((visibility("hidden")))
+
+namespace sdrk SDRK_HIDDEN {
+
+constexpr int HIST = 160;        // history samples in front of every extended f32 stream (>= 150)
+constexpr int BLK = 256;         // threads per workgroup for the streaming kernels
+constexpr int FIR_TILE = 512;    // outputs per workgroup for the 101-tap FIRs
+constexpr int DEC_STATE = 8;     // ints of RDS decoder state per channel
+
+// MFMA front end (sdr_frontend.hip): digit planes of the fixed-point taps and tap fragments
+constexpr int FT_ND = 4;
+constexpr int FT_AFRAGS = 4 * FT_ND;
+constexpr int FT_NB_DEFAULT = 32;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// sets the thread's last-error text (sdr_last_error) and returns code
+int fail(int code, const char* fmt, ...);
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) return ::sdrk::fail(SDR_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+#define LAUNCH_CHECK()                                                                              \
+    do {                                                                                            \
+        hipError_t e_ = hipGetLastError();                                                          \
+        if (e_ != hipSuccess) return ::sdrk::fail(SDR_E_HIP, "launch failed at %s:%d: %s", __FILE__, __LINE__, \
+                                                  hipGetErrorString(e_));                           \
+    } while (0)
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline size_t round_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
+
+// One PLL instance over nch channels (pll.cpp:4 arguments). A launch runs up to 2 of them
+// (blockIdx.y), so the stereo (19 kHz) and RDS (114 kHz) PLLs of a block share one dispatch.
+struct PllJob {
+    const float* in;
+    size_t in_stride;
+    float* tbuf;
+    size_t t_stride;
+    float* out;
+    size_t out_stride;
+    sdr_pll_state* st;
+    float freq, Fs, bw, ncoScale, phaseAdjust;
+    // context mode: out[0] (pll.cpp:18) is the previous block's last carrier, read by the NCO from
+    // that block's output row (prev_out[ch][n]); the PLL kernel then never touches lastCarrier, so
+    // the NCO of block b can run on another stream while the PLL of block b+1 runs.
+    const float* prev_out;
+    // pll_math.h pll_rx of every input sample (written by the producer of `in`)
+    const double* rx;
+    size_t rx_stride;
+};
+struct PllJobs {
+    PllJob j[2];
+};
+// the two parities of a persistent launch: p[0] is the parity of the launch's first block
+struct PllJobs2 {
+    PllJobs p[2];
+};
+
+// ---- sdr_frontend.hip
+struct FrontendArgs {
+    const uint8_t* iq;
+    size_t iq_stride;
+    const uint8_t* tail_in;
+    uint8_t* tail_out;
+    const float2* prev_in;
+    float2* prev_out;
+    float* fm;                 // this parity's fm_demod stream (data base)
+    const float* fm_other;     // the other parity's (history source)
+    size_t fm_stride;
+    int nch, ntaps, block_iq, block_if, D;
+    const float* h;            // plain taps (generic kernel)
+    const float* hs;           // register-blocked tap table (k_frontend2)
+    const void* afrag;         // MFMA tap fragments (fast mode)
+    double yscale;             // MFMA fixed-point scale
+    const uint32_t* pad80;     // 64 words of u8 128
+    bool fast, mfma;
+    int fe_r, fe_grid, fe_nb, fe_wpe, cus;
+};
+int frontend_launch(const FrontendArgs& a, hipStream_t s);
+
+// ---- sdr_pll.hip
+bool pll_libm_env();
+int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s);
+int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s, bool with_nco = true);
+// the context-free fmpll primitive: reciprocals, PLL, NCO
+int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
+               size_t t_stride, double* rxbuf, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale,
+               float phaseAdjust, float bw, hipStream_t s);
+// persistent PLLs: words = [pre_flag, done_count, err]; returns the number of waves in *waves
+int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
+                     unsigned long long* t0, unsigned long long* t1, uint32_t* waves, hipStream_t s);
+int launch_flag_store(uint32_t* flag, uint32_t v, hipStream_t s);
+int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStream_t s);
+int diag_pll_counts(unsigned long long* out, int reset);
+
+}  // namespace sdrk
+
+// ============================================================================================
+// Context (sdr_kernels.hip owns it; the other units see the layout)
+// ============================================================================================
+struct sdr_ctx {
+    int device = 0, nch = 0, mode = 0, rds_on = 0, flags = 0;
+    sdr_info info{};
+    int ntaps = 101;
+    // taps (device)
+    float *rf_h = nullptr, *rf_hs = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
+          *rrc_h = nullptr;
+    float *audio_pp = nullptr, *rdsbb_pp = nullptr;   // polyphase tables
+    int *audio_cnt = nullptr, *rdsbb_cnt = nullptr;
+    int audio_L = 0, rdsbb_L = 0;
+    // extended streams [2][nch][HIST + len]; pointers below are the data bases of parity 0
+    float *fm = nullptr, *sdc = nullptr, *rband = nullptr, *rdc = nullptr, *rfilt = nullptr;
+    size_t fm_stride = 0, rf_stride = 0;               // per-channel strides (if, rds lengths)
+    size_t fm_par = 0, rf_par = 0;                      // parity offsets in elements
+    // plain per-block buffers
+    float *pilot = nullptr, *band = nullptr, *gpilot = nullptr, *carrier = nullptr, *ipll = nullptr,
+          *rds_clean = nullptr, *t_st = nullptr, *t_rds = nullptr;
+    int* rds_ptq = nullptr;                             // RDS resampler (q << 8 | phase) per output
+    bool rdsbb_all101 = false;                          // every RDS polyphase row has 101 taps
+    bool audio_u1_101 = false;                          // audio resampler U == 1 with 101 taps
+    double *rx_st = nullptr, *rx_rds = nullptr;         // PLL input reciprocals (pll_math.h pll_rx),
+                                                        // [2 parities][nch][plain_stride], from the FIRs
+    size_t plain_stride = 0, pll_stride = 0, clean_stride = 0;
+    size_t plain_par = 0, pll_par = 0;                  // pilot/band/gpilot and carrier/ipll are
+                                                        // [2 parities][nch][...] so that the stages
+                                                        // split at the PLL can overlap blocks
+    // state
+    uint8_t* tail = nullptr;                            // [2][nch][2*(ntaps-1)]
+    float2* prev = nullptr;                             // [2][nch]
+    sdr_pll_state *st_pll = nullptr, *rds_pll = nullptr;
+    int32_t* dec = nullptr;                             // [nch][DEC_STATE]
+    int fe_grid = 0;                                    // front-end workgroups (0: one per tile)
+    int fe_r = 8;                                       // front-end outputs per lane (4 or 8)
+    uint32_t* pad80 = nullptr;                          // 64 words of u8 128 (the zero sample)
+    void* fe_afrag = nullptr;                           // MFMA front end: tap digit fragments
+    double fe_yscale = 0.0;                             // 2^-(F+7): fixed-point taps, x = (u-128)/128
+    bool fe_mfma = false;                               // fast mode runs k_frontend_mfma
+    int fe_nb = sdrk::FT_NB_DEFAULT;                    // MFMA front end: 16-output blocks per tile
+    int fe_wpe = 0;                                     // > 0: persistent register-prefetch MFMA front end
+    int cus = 0;                                        // compute units of the device
+    int parity = 1;                                     // parity of the current block
+    long long block = -1;                               // index of the current block
+    long long stereo_done = -1, rds_dsp_done = -1, rds_bits_done = -1, mono_done = -1;
+    long long st_pre_done = -1, st_pll_done = -1, rds_pre_done = -1, rds_pll_done = -1;
+    // persistent PLLs (sdr_plls_launch / _signal / _wait): device words [pre_flag, done_count,
+    // err], per-block timestamps of the last launch, and the host's sequence bookkeeping
+    uint32_t* pers_words = nullptr;
+    unsigned long long *pers_t0 = nullptr, *pers_t1 = nullptr;
+    int pers_tcap = 0, pers_last_n = 0;
+    uint32_t pers_launched = 0, pers_signaled = 0, pers_waves = 0;
+    uint32_t pers_base = 0;                             // sequence number of the last launch's first block
+    long long pers_first_block = -1;                    // the context block that sequence number belongs to
+    hipStream_t pers_stream = nullptr;                  // stream of the last launch
+    long long pers_block = -1;                          // block of the last signal
+    uint32_t pers_block_seq = 0;                        // its sequence number
+    std::vector<void*> allocs;
+
+    float* fm_cur() const { return fm + parity * fm_par; }
+    float* fm_oth() const { return fm + (parity ^ 1) * fm_par; }
+    float* ext(float* base, size_t par, int p) const { return base + p * par; }
+    float* plain(float* base) const { return base + parity * plain_par; }
+    float* pllbuf(float* base) const { return base + parity * pll_par; }
+    double* rxbuf(double* base) const { return base + parity * plain_par; }
+};

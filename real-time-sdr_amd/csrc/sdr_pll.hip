@@ -1,0 +1,758 @@
+// sdr_pll.hip -- the PLL / NCO recurrence of the FM/RDS hot path on MI355X (gfx950):
+//   fmpll, pll.cpp:4-61 (pllblock_args, include/pll.h:10-20), one lane per channel, with
+//   pll_math.h's correctly-rounded fast paths and double-double fallbacks;
+//   the persistent multi-block launch and its stream hand-offs.
+#include "sdr_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "pll_math.h"
+
+#pragma clang fp contract(off)
+
+namespace sdrk {
+namespace {
+// ------------------------------------------------------------------------------------------
+// PLL / NCO, pll.cpp:4-61. One lane per channel: the recurrence is serial in time.
+//
+// k_pll_libm: the literal restatement (f64 OCML atan2/sincos per step), kept as the A/B
+// reference (flag SDR_FLAG_PLL_LIBM) and used for chunk redo.
+// k_pll: the same recurrence with pll_math.h's correctly-rounded fast paths. Each 64-step chunk
+// runs branch-free; if any step of a lane reported an ambiguous f32 rounding (~6.6e-6 per step)
+// the lane restores its chunk snapshot and redoes the chunk with per-step f64-libm fallbacks.
+// Both write out[0] = lastCarrier and out[i+1] = t_i (the f32 NCO phase); k_nco_out then turns
+// t_i into cos(t_i*ncoScale + phaseAdjust) in parallel (pll.cpp:52) and updates lastCarrier.
+// ------------------------------------------------------------------------------------------
+struct PllRegs {
+    float fbI, fbQ;              // in the reduced frame: RN(cos r), RN(sin r) (pll_math.h)
+    f32x2 ip;                    // {integrator, phaseEst}: one packed multiply and add per step
+    double toff;
+    double c, s, mr;             // f64 cos r, sin r and -r of the previous step's t = q pi/2 + r
+    uint32_t nq1, b;             // 1 - q (mod 2^32) for its quadrant q, and [r < 0]
+};
+
+// The carried rotation is rebuilt from the state's previous trigArg t = (float)(w*toff + phaseEst)
+// (pll.cpp:47). The fast phase detector needs feedbackI/Q to be RN_f32(cos t), RN_f32(sin t) of
+// that same t -- true for any state this PLL (or the reference) left behind and for the initial
+// state (1, 0, toff 0, phase 0). Otherwise, or when t is out of the reduction's range, the
+// feedback is kept as given with q = 0 and mr = NaN: the first fast step yields a NaN and the
+// chunk is redone with libm fallbacks, which use the state's feedback exactly.
+__device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
+    PllRegs r;
+    r.ip = f32x2{st.integrator, st.phaseEst};
+    r.toff = st.trigOffset;
+    const float t_prev = (float)(w * r.toff + (double)r.ip.y);
+    const pllm::SinCosRN sc = pllm::sincos_rn(t_prev);
+    float fI = (float)sc.cr, fQ = (float)sc.sr;
+    pllm::rot_q(1u - sc.nq1, fI, fQ);
+    const bool consistent = (__builtin_fabs((double)t_prev) < pllm::T_MAX) && sc.tie > pllm::TIE_MIN &&
+                            fI == st.feedbackI && fQ == st.feedbackQ;
+    if (consistent) {
+        r.fbI = (float)sc.cr;
+        r.fbQ = (float)sc.sr;
+        r.c = sc.cr;
+        r.s = sc.sr;
+        r.mr = -sc.r;
+        r.nq1 = sc.nq1;
+        r.b = sc.b;
+    } else {
+        r.fbI = st.feedbackI;
+        r.fbQ = st.feedbackQ;
+        r.c = 1.0;
+        r.s = 0.0;
+        r.mr = __builtin_nan("");
+        r.nq1 = 1u;
+        r.b = 0u;
+    }
+    return r;
+}
+
+// Per-chunk proof obligations of the fast path (VGPR accumulators, one check per chunk):
+//   * every phase-detector result is at least EPS_ABS_E2 from an f32 rounding boundary (split)
+//     and |e| < pi - 2^-30 (so the wrap to [-pi, pi] is the reference's),
+//   * every cos/sin is at least 64 f64 ulps from an f32 tie (tie),
+//   * the chunk ends with |phaseEst| < 2^28, |integrator| < 2^20 (finite: a NaN or inf from an
+//     invalid input -- pll_rx gives NaN for |x| < 2^-60 -- propagates into both),
+//   * every |t| of the chunk is below 2^30 (T_MAX, the two-fma reduction's range): with the trigArg
+//     table (TAB) the launch checked |w| (|toff| + n + 1) < 1.375 * 2^29, which leaves room for
+//     |phaseEst| < 2^28 plus 16 steps of drift; without it the chunk's largest |t| is tracked.
+struct PllProof {
+    double emax = 0.0;
+    uint32_t split = 0u;
+    uint32_t tie = ~0u;
+    float tmax = 0.0f;
+};
+#ifndef SDR_PLL_HI_FIRST
+#define SDR_PLL_HI_FIRST 1
+#endif
+#ifndef SDR_PLL_PREWAIT
+#define SDR_PLL_PREWAIT 0
+#endif
+#ifndef SDR_PLL_LF_SCALAR
+#define SDR_PLL_LF_SCALAR 1   // the plain f32 loop filter (no inline asm): +1.2 %, profiles/r02/ab_pll_lf.txt
+#endif
+#ifndef SDR_PLL_EDHI
+#define SDR_PLL_EDHI 0
+#endif
+// |e| bound of the fast phase detector (the wrap to [-pi, pi] is the reference's below it)
+constexpr double PLL_EMAX = SDR_PLL_EDHI ? pllm::PI - 0x1p-30 - 0x1p-42 : pllm::PI - 0x1p-30;
+constexpr double PLL_TAB_WT_MAX = 0x1.6p29;   // |w * trigOffset| bound of the table path (above)
+
+#ifndef SDR_PLL_COUNT
+#define SDR_PLL_COUNT 0   // diagnosis build: count the fast chunks and the redone ones (sdr_diag_pll_counts)
+#endif
+#if SDR_PLL_COUNT
+// [lane-chunks, lane-chunks that failed their proof, wave-chunks, wave-chunks redone]
+__device__ unsigned long long g_pll_counts[4];
+__device__ __forceinline__ void pll_count_chunk(bool ok) {
+    const unsigned long long exec = __builtin_amdgcn_read_exec();
+    const unsigned long long bad = __ballot(!ok) & exec;
+    if ((int)__lane_id() == __ffsll((long long)exec) - 1) {
+        atomicAdd(&g_pll_counts[0], (unsigned long long)__popcll(exec));
+        atomicAdd(&g_pll_counts[1], (unsigned long long)__popcll(bad));
+        atomicAdd(&g_pll_counts[2], 1ull);
+        atomicAdd(&g_pll_counts[3], bad ? 1ull : 0ull);
+    }
+}
+#endif
+
+// TAB: the trigArg offsets come from a table whose range the kernel checked once (pll_run)
+template <bool TAB>
+__device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
+    return (pf.emax < PLL_EMAX) & (pf.split == 0u) & (pf.tie > pllm::TIE_MIN) &
+           (__builtin_fabs(r.ip.y) < 0x1p28f) & (__builtin_fabs(r.ip.x) < 0x1p20f) &
+           (TAB || (pf.tmax < 0x1p30f));
+}
+
+// the f64 libm results of the reference step (pll.cpp:39, :49-50), out of line: only the rare
+// fallbacks call them, and the unrolled redo chunks stay small. They return glibc's value RN64(f)
+// from double-double evaluations (pll_math.h), not the device libm's, which differs from glibc by
+// 1-2 ulps on 3-27% of inputs -- enough to flip an f32 rounding on the near-midpoint inputs that
+// reach a fallback. |t| >= 2^30 (a stream past ~25 min for the 114 kHz PLL) reduces by
+// Payne-Hanek in double-double (pll_math.h dd_reduce_f32_large); only inf/NaN keep the device libm.
+__device__ __noinline__ float pll_atan2_ref(float eQ, float eI) {
+    return (float)pllm::dd_atan2_f32(eQ, eI, atan2((double)eQ, (double)eI));
+}
+__device__ __noinline__ void pll_sincos_ref(float t, double* s, double* c) {
+    if (__builtin_fabs(t) <= 3.4028234663852886e38f)
+        pllm::dd_sincos_f32(t, s, c);
+    else
+        sincos((double)t, s, c);
+}
+
+// split accumulator of the phase detector's rounding test, per step: acc | (lo ^ hi) as ONE
+// v_bitop3_b32 (truth table 0xF6 = s0 | (s1 ^ s2)). Written out because the compiler otherwise
+// keeps all 16 (lo, hi) pairs of a chunk alive and compares them at its end.
+__device__ __forceinline__ uint32_t or_xor(uint32_t acc, uint32_t lo, uint32_t hi) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xf6" : "=v"(d) : "v"(acc), "v"(lo), "v"(hi));
+    return d;
+}
+
+// tie accumulator: min(acc, tc, ts) as one v_min3_u32 (the compiler otherwise pairs the keys of
+// consecutive steps into a v_min_u32 + v_min3_u32 tree)
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+// One step of pll.cpp:36-50. CHECKED: every result the fast path cannot prove is recomputed
+// with the f64 libm exactly as the reference (used for chunk redo and short tails).
+template <bool CHECKED, bool TAB>
+__device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float Kp, float Ki, double w, double wt,
+                                         float& t_out, PllProof& pf) {
+    // pll.cpp:36-37 in the reduced frame, as one packed multiply: x * (fbI, -fbQ)
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v fb = {r.fbI, -r.fbQ};
+    const f2v ee = x * fb;
+    const float eI0 = ee.x, eQ0 = ee.y;
+    // pll.cpp:39: atan2(eQ, eI) = base + Y/X (pll_math.h phase_detect2), rounding proven below
+    const double base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
+    const double Y = pllm::fma_((double)eI0, r.s, (double)eQ0 * r.c);
+#if SDR_PLL_EDHI
+    // the bracket ed -/+ eps as fma(Y, rx, base -/+ eps): base -/+ eps is ready before the input,
+    // so the rounded e is one operation closer to Y (same proof: each end moves < 2^-50.5, far
+    // inside eps - |error of ed|); |ed| <= |ed + eps| + 2^-43 for the range test
+    const double ed = pllm::fma_(Y, rx, base + pllm::EPS_ABS_E2);
+    const float lo = (float)pllm::fma_(Y, rx, base - pllm::EPS_ABS_E2), hi = (float)ed;
+#else
+    const double ed = pllm::fma_(Y, rx, base);
+#if SDR_PLL_HI_FIRST
+    // hi (the value used) first: the loop filter's packed product can issue while lo, the range
+    // and the split test fill its hazard wait states
+    const float hi = (float)(ed + pllm::EPS_ABS_E2);
+    const float lo = (float)(ed - pllm::EPS_ABS_E2);
+#else
+    const float lo = (float)(ed - pllm::EPS_ABS_E2), hi = (float)(ed + pllm::EPS_ABS_E2);
+#endif
+#endif
+    float e = hi;                                             // = RN32(ed) whenever lo == hi
+    if (CHECKED) {
+        if (!((__builtin_fabs(ed) < PLL_EMAX) && lo == hi)) {
+            float a = eI0, b = -eQ0;                          // eI - i eQ = i^q (eI0 - i eQ0)
+            pllm::rot_q(1u - r.nq1, a, b);
+            e = pll_atan2_ref(-b, a);                         // pll.cpp:39
+        }
+    } else {
+        pf.emax = fmax(pf.emax, __builtin_fabs(ed));
+        pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+    }
+    // pll.cpp:41-42: integ += Ki e; phaseEst = (phaseEst + Kp e) + integ, with the two products
+    // and the two first sums as one v_pk_mul_f32 + one v_pk_add_f32 (the same f32 roundings)
+#if SDR_PLL_LF_SCALAR
+    // scalar f32: 5 VALU, and no hazard wait states after packed-f32 results
+    {
+        float ki_e = Ki * e;
+        if (SDR_PLL_LF_SCALAR == 2) asm("" : "+v"(ki_e));      // keeps the SLP vectoriser from packing
+        const float integ = r.ip.x + ki_e;
+        r.ip.y = (r.ip.y + Kp * e) + integ;
+        r.ip.x = integ;
+    }
+#else
+    r.ip = r.ip + f32x2{Ki, Kp} * f32x2{e, e};
+    float ph = r.ip.y;                                        // in place (else a pk_add + move)
+    asm("v_add_f32 %0, %0, %1" : "+v"(ph) : "v"(r.ip.x));
+    r.ip.y = ph;
+#endif
+    float t;
+    if (TAB) {                                                // wt = w * trigOffset, tabulated
+        t = (float)(wt + (double)r.ip.y);                     // pll.cpp:47
+    } else {
+        r.toff += 1.0;                                        // pll.cpp:46
+        t = (float)(w * r.toff + (double)r.ip.y);             // pll.cpp:47
+    }
+    const pllm::SinCosRN sc = pllm::sincos_rn(t);
+    r.c = sc.cr;
+    r.s = sc.sr;
+    r.mr = -sc.r;
+    r.nq1 = sc.nq1;
+    r.b = sc.b;
+    r.fbI = (float)sc.cr;                                     // pll.cpp:49-50, reduced frame
+    r.fbQ = (float)sc.sr;
+    if (CHECKED) {
+        const bool in_range = __builtin_fabs((double)t) < pllm::T_MAX;
+        if (!(in_range && sc.tie > pllm::TIE_MIN)) {
+            double sv, cv;
+            pll_sincos_ref(t, &sv, &cv);
+            pllm::rot_q(r.nq1 - 1u, cv, sv);                  // into the reduced frame, exactly
+            r.fbI = (float)cv;
+            r.fbQ = (float)sv;
+            r.c = cv;
+            r.s = sv;
+            if (!in_range) r.mr = __builtin_nan("");
+        }
+    } else {
+        pf.tie = min3_u32(pf.tie, sc.tc, sc.ts);
+        if (!TAB) pf.tmax = fmaxf(pf.tmax, __builtin_fabsf(t));
+    }
+    t_out = t;
+}
+
+#ifndef SDR_PLL_CHUNK
+#define SDR_PLL_CHUNK 16
+#endif
+constexpr int PLL_CHUNK = SDR_PLL_CHUNK;
+#ifndef SDR_PLL_W01
+#define SDR_PLL_W01 0
+#endif
+#ifndef SDR_PLL_NBUF
+#define SDR_PLL_NBUF 2
+#endif
+constexpr int PLL_NBUF = SDR_PLL_NBUF;   // register buffers of inputs (prefetch distance NBUF - 1 chunks)
+
+// VEC: x / rx rows and the t buffer are 16-byte aligned with strides that are multiples of 4
+// (x, t) and 2 (rx), so a chunk's inputs are prefetched with 16-byte loads one chunk ahead and
+// the 16 phases are stored with 16-byte stores -- the unrolled chunk itself touches no memory.
+// One lane per channel runs the n serial steps of one PllJob.
+// TAB: every lane of the wave has the same trigOffset (a context's channels advance together), so
+// w * trigOffset of every step comes from a table the wave builds in LDS up front (pll.cpp:46-47
+// evaluated once per step index instead of once per channel and step).
+template <bool VEC, bool TAB>
+__device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const double* __restrict__ wtab) {
+    const float* __restrict__ in = jb.in;
+    const size_t in_stride = jb.in_stride, t_stride = jb.t_stride, out_stride = jb.out_stride;
+    float* __restrict__ tbuf = jb.tbuf;
+    float* __restrict__ out = jb.out;
+    sdr_pll_state* __restrict__ st = jb.st;
+    const float freq = jb.freq, Fs = jb.Fs, normBandwidth = jb.bw;
+    const float Cp = 2.666;
+    const float Ci = 3.555;
+    const float Kp = normBandwidth * Cp;
+    const float Ki = normBandwidth * normBandwidth * Ci;
+    const double w = 2 * 3.14159265358979323846 * (freq / Fs);
+    const sdr_pll_state s0 = st[ch];
+    const float* x = in + (size_t)ch * in_stride;
+    const double* rxp = jb.rx + (size_t)ch * jb.rx_stride;
+    float* tb = tbuf + (size_t)ch * t_stride;
+    if (!jb.prev_out) out[(size_t)ch * out_stride] = s0.lastCarrier;   // pll.cpp:18
+    PllRegs r = pll_load(s0, w);
+    // Chunks rotate through PLL_NBUF register buffers: chunk c computes from buffer c % NBUF, stores
+    // its phases, then refills that buffer with chunk c + NBUF. A chunk's inputs are thus loaded
+    // NBUF - 1 chunks ahead and, being issued after the previous chunk's stores, never make a
+    // wait include those stores (vmcnt counts loads and stores in issue order). The main loop
+    // covers a multiple of NBUF chunks; the rest (< NBUF chunks + n % CHUNK) runs checked steps.
+    constexpr int C = PLL_CHUNK, NB = PLL_NBUF;
+    const int nchunks = n / C;
+    const int nmain = nchunks - nchunks % NB;
+    float xb[NB][C];
+    double rb[NB][C];
+    auto load_chunk = [&](float* dx, double* dr, int i0) {
+        if (VEC) {
+#pragma unroll
+            for (int k = 0; k < C / 4; k++) {
+                const float4 v = reinterpret_cast<const float4*>(x + i0)[k];
+                dx[4 * k] = v.x; dx[4 * k + 1] = v.y; dx[4 * k + 2] = v.z; dx[4 * k + 3] = v.w;
+            }
+#pragma unroll
+            for (int k = 0; k < C / 2; k++) {
+                const double2 v = reinterpret_cast<const double2*>(rxp + i0)[k];
+                dr[2 * k] = v.x; dr[2 * k + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < C; k++) {
+                dx[k] = x[i0 + k];
+                dr[k] = rxp[i0 + k];
+            }
+        }
+    };
+    if (nmain > 0) {
+#pragma unroll
+        for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
+#if SDR_PLL_PREWAIT
+        // the first buffers land before the loop (one memory latency per block). Otherwise the
+        // compiler's wait counts at the loop header merge these loads' positions with the back
+        // edge's and the steady-state loop waits for loads and stores it does not need: vmcnt(4)
+        // before every refill (the previous chunk's refill) and vmcnt(12) inside every chunk (the
+        // stores just issued), exposing a memory latency per chunk.
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt and lgkmcnt unconstrained (gfx9)
+#endif
+    }
+#if SDR_PLL_W01
+    double2 w01 = TAB ? reinterpret_cast<const double2*>(wtab)[0] : double2{0.0, 0.0};
+#endif
+    for (int c0 = 0; c0 < nmain; c0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; u++) {
+            const int i0 = (c0 + u) * C;
+            double wv[C];
+            if (TAB) {
+                // the first two steps' table entries were read at the end of the previous chunk
+                // (w01), so the chunk's first steps do not wait on the LDS latency
+#if SDR_PLL_W01
+                wv[0] = w01.x; wv[1] = w01.y;
+#pragma unroll
+                for (int k = 1; k < C / 2; k++) {
+#else
+#pragma unroll
+                for (int k = 0; k < C / 2; k++) {
+#endif
+                    const double2 v = reinterpret_cast<const double2*>(wtab + i0)[k];
+                    wv[2 * k] = v.x; wv[2 * k + 1] = v.y;
+                }
+            }
+            const PllRegs snap = r;
+            PllProof pf;
+            float tv[C];
+#pragma unroll
+            for (int j = 0; j < C; j++)
+                pll_step<false, TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
+            const bool chunk_ok = pll_chunk_ok<TAB>(pf, r, w, C);
+#if SDR_PLL_COUNT
+            pll_count_chunk(chunk_ok);
+#endif
+            if (!chunk_ok) {
+                r = snap;
+#pragma unroll
+                for (int j = 0; j < C; j++)
+                    pll_step<true, TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
+            }
+            if (VEC) {
+#pragma unroll
+                for (int k = 0; k < C / 4; k++)
+                    reinterpret_cast<float4*>(tb + i0)[k] = make_float4(tv[4 * k], tv[4 * k + 1], tv[4 * k + 2], tv[4 * k + 3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
+            }
+            // refill (the last refills re-read the final chunk: harmless, keeps the loop branch-free)
+#if SDR_PLL_DIAG_L2
+            // diagnosis only (wrong results): every refill re-reads the first chunks (L2-resident),
+            // to measure what the HBM latency of the refills costs
+            load_chunk(xb[u], rb[u], u * C);
+#else
+            load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
+#endif
+#if SDR_PLL_W01
+            if (TAB) w01 = reinterpret_cast<const double2*>(wtab)[min(i0 + C, n - 2) >> 1];
+#endif
+        }
+    }
+    {
+        // the rest (< NB chunks + n % C steps), checked, from register buffers loaded one piece
+        // ahead (one exposed memory latency for the whole rest instead of one per step)
+        PllProof pf;
+        const int i_rest = nmain * C;
+        float xr[C];
+        double rr[C], wr[C];
+        auto load_rest = [&](int i0) {
+#pragma unroll
+            for (int k = 0; k < C; k++) {
+                const int i = min(i0 + k, n - 1);
+                xr[k] = x[i];
+                rr[k] = rxp[i];
+                wr[k] = TAB ? wtab[i] : 0.0;
+            }
+        };
+        if (i_rest < n) load_rest(i_rest);
+        for (int i0 = i_rest; i0 < n; i0 += C) {
+            float xc[C];
+            double rc[C], wc[C];
+#pragma unroll
+            for (int k = 0; k < C; k++) { xc[k] = xr[k]; rc[k] = rr[k]; wc[k] = wr[k]; }
+            if (i0 + C < n) load_rest(i0 + C);
+#pragma unroll
+            for (int k = 0; k < C; k++)
+                if (i0 + k < n) pll_step<true, TAB>(r, xc[k], rc[k], Kp, Ki, w, wc[k], tb[i0 + k], pf);
+        }
+    }
+    if (TAB) r.toff = s0.trigOffset + (double)n;               // pll.cpp:46, n times (exact)
+    // every field but lastCarrier (k_nco_out's); the feedback back in the frame of t
+    pllm::rot_q(1u - r.nq1, r.fbI, r.fbQ);
+    st[ch].feedbackI = r.fbI;
+    st[ch].feedbackQ = r.fbQ;
+    st[ch].integrator = r.ip.x;
+    st[ch].phaseEst = r.ip.y;
+    st[ch].trigOffset = r.toff;
+}
+
+// VEC: x / rx rows and the t buffer are 16-byte aligned with strides that are multiples of 4
+// (x, t) and 2 (rx), so a chunk's inputs are prefetched with 16-byte loads and the 16 phases are
+// stored with 16-byte stores -- the unrolled chunk itself touches no memory.
+// Dynamic LDS: n doubles when the launch allows the trigArg table (launch_plls), else none.
+template <bool VEC>
+__global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, int tab_ok) {
+    extern __shared__ double wtab[];
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;   // lane 0 always holds a channel
+    const bool active = ch < nch;
+    const PllJob& jb = jobs.j[blockIdx.y];
+    // the serial PLL bounds every block-step: let its waves win issue arbitration on shared SIMDs
+    __builtin_amdgcn_s_setprio(3);
+    const double toff0 = active ? jb.st[ch].trigOffset : 0.0;
+    const double w = 2 * 3.14159265358979323846 * (jb.freq / jb.Fs);
+    // one wave per workgroup: the table is valid when all channels of the wave share trigOffset
+    // and every w * trigOffset of the launch stays below 2^29 (so |t| < 2^30 whenever
+    // |phaseEst| < 2^28). All 64 lanes build it, then the lanes without a channel leave.
+    const double toff_l0 = __shfl(toff0, 0);
+    const bool tab = tab_ok && __all(!active || toff0 == toff_l0) &&
+                     __builtin_fabs(w) * (__builtin_fabs(toff_l0) + (double)n + 1.0) < PLL_TAB_WT_MAX;
+    if (tab) {
+        for (int k = threadIdx.x; k < n; k += 64) wtab[k] = w * (toff_l0 + (double)(k + 1));   // pll.cpp:46-47
+        __syncthreads();
+    }
+    if (!active) return;
+    if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
+    else pll_run<VEC, false>(jb, n, ch, nullptr);
+}
+
+// ------------------------------------------------------------------------------------------
+// Persistent PLLs (sdr_plls_launch / _signal / _wait): one dispatch runs the PLLs of `nblocks`
+// consecutive blocks, so consecutive blocks are not separated by a dispatch (the ~19 us gap
+// between back-to-back k_pll launches). Before block j the waves wait, with an
+// agent-scope acquire, for the front-end stream's flag (k_flag_store, dispatched after the
+// pre-PLL kernels of that block); after it each wave adds 1 to a done counter with an
+// agent-scope release, which the post stream waits on (k_flag_wait). hipStreamWriteValue32 is
+// not used for the flag: in a first version its write overtook the still-running pre-PLL kernel
+// (the first block of a launch, whose waves are already waiting, read inputs before they were
+// complete), while a kernel dispatch starts only after its predecessor has completed. Blocks alternate
+// the context's two buffer parities. Every wait is bounded: after PLL_WAIT_TICKS of the 100 MHz
+// clock the launch records an error and completes its remaining blocks without computing, so no
+// wave and no waiting stream can hang.
+// ------------------------------------------------------------------------------------------
+constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrealtime
+
+template <bool VEC>
+__global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
+                                                  const uint32_t* pre_flag, uint32_t pre_first,
+                                                  uint32_t* done_count, uint32_t* err,
+                                                  unsigned long long* t_start, unsigned long long* t_end,
+                                                  int sys_acquire) {
+    extern __shared__ double wtab[];
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = ch < nch;
+    __builtin_amdgcn_s_setprio(3);
+    bool dead = false;
+    for (int j = 0; j < nblocks; j++) {
+        const PllJob& jb = jobs.p[j & 1].j[blockIdx.y];   // p[0]: the parity of the launch's first block
+        if (!dead) {
+            const uint32_t want = pre_first + (uint32_t)j + 1u;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while ((int32_t)((sys_acquire ? __hip_atomic_load(pre_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : __hip_atomic_load(pre_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) -
+                             want) < 0) {
+                __builtin_amdgcn_s_sleep(4);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
+                    dead = true;
+                    break;
+                }
+            }
+            if (dead && threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!dead) {
+            if (threadIdx.x == 0)
+                __hip_atomic_fetch_min(t_start + j, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double toff0 = active ? jb.st[ch].trigOffset : 0.0;
+            const double w = 2 * 3.14159265358979323846 * (jb.freq / jb.Fs);
+            const double toff_l0 = __shfl(toff0, 0);
+            const bool tab = tab_ok && __all(!active || toff0 == toff_l0) &&
+                             __builtin_fabs(w) * (__builtin_fabs(toff_l0) + (double)n + 1.0) < PLL_TAB_WT_MAX;
+            if (tab) {
+                for (int k = threadIdx.x; k < n; k += 64) wtab[k] = w * (toff_l0 + (double)(k + 1));   // pll.cpp:46-47
+                __syncthreads();
+            }
+            if (active) {
+                if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
+                else pll_run<VEC, false>(jb, n, ch, nullptr);
+            }
+            __syncthreads();   // every lane's table reads and state/phase stores issued before the release
+        }
+        if (threadIdx.x == 0) {
+            if (!dead)
+                __hip_atomic_fetch_max(t_end + j, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(done_count, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// The two ends of the persistent PLLs' hand-offs, as one-wave kernels so that HIP's in-order
+// kernel dispatch (each dispatch starts after the previous one in its stream has completed and
+// released its writes) orders them: k_flag_store publishes "block ready" after the pre-PLL
+// kernels of the front-end stream; k_flag_wait holds the post stream until the PLL waves have
+// released a block (bounded, like the PLL's own waits).
+__global__ void k_flag_store(uint32_t* flag, uint32_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void k_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int32_t)(__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+        __builtin_amdgcn_s_sleep(4);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
+            __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+    }
+}
+
+// pll_rx of a PLL input with no fused producer (the batched sdr_fmpll primitive)
+__global__ __launch_bounds__(BLK) void k_pll_rx(double* __restrict__ rx, size_t rx_stride, const float* __restrict__ x,
+                                                size_t x_stride, int n) {
+    const int ch = blockIdx.y;
+    const int i = blockIdx.x * BLK + threadIdx.x;
+    if (i < n) rx[(size_t)ch * rx_stride + i] = pllm::pll_rx(x[(size_t)ch * x_stride + i]);
+}
+
+__global__ __launch_bounds__(64) void k_pll_libm(const PllJobs jobs, int n, int nch) {
+    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= nch) return;
+    const PllJob& jb = jobs.j[blockIdx.y];
+    const float* __restrict__ in = jb.in;
+    const size_t in_stride = jb.in_stride, t_stride = jb.t_stride, out_stride = jb.out_stride;
+    float* __restrict__ tbuf = jb.tbuf;
+    float* __restrict__ out = jb.out;
+    sdr_pll_state* __restrict__ st = jb.st;
+    const float freq = jb.freq, Fs = jb.Fs, normBandwidth = jb.bw;
+    const float Cp = 2.666;
+    const float Ci = 3.555;
+    const float Kp = normBandwidth * Cp;
+    const float Ki = normBandwidth * normBandwidth * Ci;
+    const double w = 2 * 3.14159265358979323846 * (freq / Fs);  // 2*PI*(freq/Fs), pll.cpp:47
+    sdr_pll_state s = st[ch];
+    const float* x = in + (size_t)ch * in_stride;
+    if (!jb.prev_out) out[(size_t)ch * out_stride] = s.lastCarrier;
+    float* o = tbuf + (size_t)ch * t_stride;
+    float fbI = s.feedbackI, fbQ = s.feedbackQ, integ = s.integrator, ph = s.phaseEst;
+    double toff = s.trigOffset;
+    for (int i = 0; i < n; i++) {
+        const float xi = x[i];
+        const float eI = xi * fbI;
+        const float eQ = xi * (-fbQ);
+        const float e = (float)atan2((double)eQ, (double)eI);
+        integ = integ + Ki * e;
+        ph = ph + Kp * e + integ;
+        toff += 1.0;
+        const float t = (float)(w * toff + (double)ph);
+        double sv, cv;
+        sincos((double)t, &sv, &cv);
+        fbI = (float)cv;
+        fbQ = (float)sv;
+        o[i] = t;
+    }
+    s.feedbackI = fbI;
+    s.feedbackQ = fbQ;
+    st[ch].feedbackI = fbI;
+    st[ch].feedbackQ = fbQ;
+    st[ch].integrator = integ;
+    st[ch].phaseEst = ph;
+    st[ch].trigOffset = toff;
+}
+
+// glibc's cos of pll.cpp:52 for the inputs the fast path cannot decide (see pll_atan2_ref)
+__device__ __noinline__ float nco_cos_ref(float a) {
+    double sv, cv;
+    pll_sincos_ref(a, &sv, &cv);
+    return (float)cv;
+}
+
+// out[ch][i+1]: t_i -> (float)cos((double)(t_i*ncoScale + phaseAdjust)) (pll.cpp:52), in parallel;
+// lastCarrier <- out[ch][n] (pll.cpp:58)
+__global__ __launch_bounds__(BLK) void k_nco_out(const PllJobs jobs, int n) {
+    const int ch = blockIdx.y;
+    const int i = blockIdx.x * BLK + threadIdx.x;
+    if (i >= n) return;
+    const PllJob& jb = jobs.j[blockIdx.z];
+    const float* __restrict__ tbuf = jb.tbuf;
+    const size_t t_stride = jb.t_stride, out_stride = jb.out_stride;
+    float* __restrict__ out = jb.out;
+    sdr_pll_state* __restrict__ st = jb.st;
+    const float ncoScale = jb.ncoScale, phaseAdjust = jb.phaseAdjust;
+    float* o = out + (size_t)ch * out_stride + 1;
+    const float t = tbuf[(size_t)ch * t_stride + i];
+    const float a = t * ncoScale + phaseAdjust;
+    const pllm::SinCos sc = pllm::sincos_f32(a);
+    float v = (float)sc.c;
+    if (!sc.ok) v = nco_cos_ref(a);
+    o[i] = v;
+    if (i == n - 1) st[ch].lastCarrier = v;
+    if (i == 0 && jb.prev_out) o[-1] = jb.prev_out[(size_t)ch * out_stride + n];
+}
+// PLL + NCO output: k_pll (fast, default) or k_pll_libm (SDR_FLAG_PLL_LIBM / env SDR_PLL=libm)
+}  // namespace
+
+bool pll_libm_env() {
+    static const bool v = [] {
+        const char* e = std::getenv("SDR_PLL");
+        return e && std::strcmp(e, "libm") == 0;
+    }();
+    return v;
+}
+
+namespace {
+// SDR_PLL_TAB=0: per-lane trigArg offsets (A/B of the LDS table)
+bool pll_notab_env() {
+    static const bool v = [] {
+        const char* e = std::getenv("SDR_PLL_TAB");
+        return e && std::strcmp(e, "0") == 0;
+    }();
+    return v;
+}
+
+}  // namespace
+
+int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
+    if (n > 0) {
+        hipLaunchKernelGGL(k_nco_out, dim3(cdiv(n, BLK), nch, njobs), dim3(BLK), 0, s, jobs, n);
+        LAUNCH_CHECK();
+    }
+    return SDR_OK;
+}
+
+int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s, bool with_nco) {
+    const dim3 g(cdiv(nch, 64), njobs), b(64);
+    bool vec = true;
+    for (int k = 0; k < njobs; k++) {
+        const PllJob& j = jobs.j[k];
+        vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
+              (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
+              (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0);
+    }
+    // LDS table of w * trigOffset (k_pll): n doubles, 16-byte rows
+    const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
+    const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
+    const size_t lds = tab_ok ? tab_bytes : 0;
+    if (libm || pll_libm_env()) {
+        hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, jobs, n, nch);
+    } else if (vec) {
+        hipLaunchKernelGGL(k_pll<true>, g, b, lds, s, jobs, n, nch, tab_ok);
+    } else {
+        hipLaunchKernelGGL(k_pll<false>, g, b, lds, s, jobs, n, nch, tab_ok);
+    }
+    LAUNCH_CHECK();
+    return with_nco ? launch_nco(jobs, njobs, n, nch, s) : SDR_OK;
+}
+
+int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
+               size_t t_stride, double* rxbuf, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale,
+               float phaseAdjust, float bw, hipStream_t s) {
+    if (n > 0) {
+        hipLaunchKernelGGL(k_pll_rx, dim3(cdiv(n, BLK), nch), dim3(BLK), 0, s, rxbuf, t_stride, in, in_stride, n);
+        LAUNCH_CHECK();
+    }
+    PllJobs jobs{};
+    jobs.j[0] = PllJob{in, in_stride, tbuf, t_stride, out, out_stride, st, freq, Fs, bw, ncoScale, phaseAdjust, nullptr,
+                       rxbuf, t_stride};
+    return launch_plls(libm, jobs, 1, n, nch, s);
+}
+
+int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
+                     unsigned long long* t0, unsigned long long* t1, uint32_t* waves, hipStream_t s) {
+    bool vec = true;
+    for (int k = 0; k < 2; k++)
+        for (int q = 0; q < 2; q++) {
+            const PllJob& j = jobs.p[k].j[q];
+            vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
+                  (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
+                  (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0);
+        }
+    const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
+    const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
+    const dim3 g(cdiv(nch, 64), 2), b(64);
+    *waves = g.x * g.y;
+    const char* acq = std::getenv("SDR_PLL_ACQUIRE");   // diagnosis: system-scope acquire
+    const int sys_acq = (acq && std::strcmp(acq, "system") == 0) ? 1 : 0;
+    if (vec)
+        hipLaunchKernelGGL(k_pll_multi<true>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
+                           words, pre_first, words + 1, words + 2, t0, t1, sys_acq);
+    else
+        hipLaunchKernelGGL(k_pll_multi<false>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
+                           words, pre_first, words + 1, words + 2, t0, t1, sys_acq);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+int launch_flag_store(uint32_t* flag, uint32_t v, hipStream_t s) {
+    hipLaunchKernelGGL(k_flag_store, dim3(1), dim3(64), 0, s, flag, v);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStream_t s) {
+    hipLaunchKernelGGL(k_flag_wait, dim3(1), dim3(64), 0, s, ctr, want, err);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+
+// Diagnosis builds only (-DSDR_PLL_COUNT=1): the PLL chunk counters [lane-chunks, failed lane-chunks,
+// wave-chunks, redone wave-chunks], optionally reset; -1 in product builds.
+int diag_pll_counts(unsigned long long* out, int reset) {
+#if SDR_PLL_COUNT
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pll_counts), sizeof(unsigned long long) * 4));
+    if (reset) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pll_counts), z, sizeof z));
+    }
+    return SDR_OK;
+#else
+    (void)out;
+    (void)reset;
+    return -1;
+#endif
+}
+
+}  // namespace sdrk

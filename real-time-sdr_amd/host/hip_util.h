@@ -50,7 +50,8 @@ inline hipStream_t thread_stream() {
         hipStream_t s = nullptr;
         S() { check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate"); }
         ~S() {
-            if (s) (void)hipStreamDestroy(s);
+            // sdr_stream_destroy also frees the per-stream sdr_fmpll scratch cached for this handle
+            if (s) (void)sdr_stream_destroy(s);
         }
     } st;
     return st.s;

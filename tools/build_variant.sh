@@ -5,5 +5,6 @@ name=$1; shift
 mkdir -p build/variants
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-flush-denormals-to-zero \
   -mllvm -pragma-unroll-threshold=1000000 -Iinclude "$@" -shared -Wl,-soname,libsdr_amd.so \
-  -o build/variants/$name.so real-time-sdr_amd/csrc/sdr_kernels.hip real-time-sdr_amd/csrc/sdr_taps.cpp
+  -o build/variants/$name.so real-time-sdr_amd/csrc/sdr_kernels.hip real-time-sdr_amd/csrc/sdr_frontend.hip \
+  real-time-sdr_amd/csrc/sdr_pll.hip real-time-sdr_amd/csrc/sdr_taps.cpp
 echo build/variants/$name.so
