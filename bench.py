@@ -144,7 +144,7 @@ class GpuStepper:
         import torch
         self.torch = torch
         self.pkg = pkg = _load_pkg()
-        self.args, self.nch, self.nblocks = args, nch, nblocks
+        self.args, self.nch, self.nblocks, self.first = args, nch, nblocks, first
         self.dev = dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
         self.iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
@@ -176,8 +176,16 @@ class GpuStepper:
         self.s_fe, self.s_pll, self.s_post = s_fe, s_pll, s_post
         # SDR_BENCH_PLL=persistent (default): one PLL dispatch per phase (warm-up, timed) that waits
         # for each block's device flag (sdr_plls_launch/_signal/_wait); "dispatch": one sdr_plls
-        # dispatch per block, ordered by events
-        self.persist = os.environ.get("SDR_BENCH_PLL", "persistent") == "persistent"
+        # dispatch per block, ordered by events. The persistent kernel's waves spin until a later
+        # dispatch on the front-end stream publishes the block, so it may only run where that
+        # dispatch cannot queue behind it: the PLL stream must own its hardware queue. A CU-masked
+        # stream does (the runtime gives every stream with a CU mask a dedicated HSA queue instead
+        # of sharing one from the pool), plain streams do not (GPU_MAX_HW_QUEUES = 4 pool queues are
+        # shared by the torch streams, the gather stream and RCCL's): without masks -> dispatch.
+        want = os.environ.get("SDR_BENCH_PLL", "persistent")
+        self.persist = want == "persistent" and bool(self.created)
+        self.pll_mode = ("persistent" if self.persist else "dispatch") + (
+            "" if want != "persistent" or self.persist else " (no CU-masked streams: persistent PLL not safe)")
         self.s_gather = torch.cuda.Stream(dev)       # torch pool streams are non-blocking
         self.mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
         self.lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]
@@ -197,7 +205,7 @@ class GpuStepper:
         self.cap_lr = torch.empty(nblocks, nv, 2 * info.n_audio, dtype=torch.int16, device=dev)
         self.cap_bits = torch.empty(nblocks, nv, pkg.SDR_MAX_BITS, dtype=torch.uint8, device=dev)
         self.cap_nbits = torch.empty(nblocks, nv, dtype=torch.int32, device=dev)
-        self.gathering = False
+        self.cap_g = None           # receiving rank: the same rows of every rank's gathered block
 
     def outputs_spec(self):
         return {"lr": ((self.nch, 2 * self.info.n_audio), self.torch.int16),
@@ -249,8 +257,33 @@ class GpuStepper:
             # stream so that the masked (blocking) streams never meet null-stream work
             with torch.cuda.stream(self.s_gather):
                 self.s_gather.wait_event(self.post_done[b])
-                gather(lr=lr, bits=bits)
+                got = gather(lr=lr, bits=bits)
+                if got is not None:
+                    self._capture_gathered(b, got)
                 self.gather_done[b].record(self.s_gather)
+
+    def _capture_gathered(self, b: int, got: dict) -> None:
+        """Receiving rank: rows vsel of every rank's gathered lr / bits of block b, kept for the check
+        after the timed region (the gather buffers are reused every block-step)."""
+        torch = self.torch
+        world = len(got["lr"])
+        d = got["lr"][0].device
+        if self.cap_g is None:
+            nv = self.vsel.numel()
+            self.vsel_g = self.vsel.to(d)
+            self.cap_g = {k: torch.empty((self.nblocks, world, nv) + tuple(got[k][0].shape[1:]), dtype=got[k][0].dtype,
+                                         device=d) for k in ("lr", "bits")}
+        for k in ("lr", "bits"):
+            for r in range(world):
+                torch.index_select(got[k][r], 0, self.vsel_g, out=self.cap_g[k][b, r])
+
+    def gathered_digests(self) -> list | None:
+        """Receiving rank: per source rank, the digest of its gathered rows (compared with the digest
+        the source rank computes over its own outputs, captured()['digest'])."""
+        if self.cap_g is None:
+            return None
+        lr, bits = self.cap_g["lr"].cpu().numpy(), self.cap_g["bits"].cpu().numpy()
+        return [_digest(lr[:, r], bits[:, r]) for r in range(lr.shape[1])]
 
     def synchronize(self) -> None:
         self.torch.cuda.synchronize(self.dev)
@@ -261,8 +294,10 @@ class GpuStepper:
         rng = range(warmup, self.nblocks)
         fe_avg_s = float(np.mean([self.fe_start[b].elapsed_time(self.fe_end[b]) for b in rng])) / 1e3
         fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
+        cyc = None
         if self.persist:   # device-clock time of each block inside the timed phase's dispatch
             pll_ms = float(np.mean(self.pipe.plls_report(stream=self.s_pll)))
+            cyc = self.pipe.plls_cycles(stream=self.s_pll)   # the waves' own shader-clock count
         else:
             pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
         achieved = fe_bytes / fe_avg_s / 1e9
@@ -278,10 +313,29 @@ class GpuStepper:
                               ", stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial chains",
                     "bound": "serial recurrence: block_if dependent steps per chain, one lane per chain "
                              "(per-wave VALU issue, DESIGN.md 4a)",
+                    "mode": self.pll_mode,
                     "avg_launch_ms": round(pll_ms, 4), "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
                     "share_of_step": round(pll_ms / (elapsed / steps * 1e3), 4),
+                    **self._pll_issue(cyc),
                     **({"chunk_redo": redo} if redo else {})},
         }
+
+    @staticmethod
+    def _pll_issue(cyc) -> dict:
+        """The PLL's efficiency against its bound (one wave per SIMD issues one VALU per quad-cycle):
+        VALU instructions per step from the committed counters, cycles per step measured live by the
+        waves' own s_memtime, and issue_frac = 4 x VALU per step / cycles per step."""
+        out = {}
+        pc = _pll_counters()
+        if cyc is not None and cyc[0] > 0:
+            out["cycles_per_step"] = round(cyc[0], 1)
+            out["shader_clock_mhz"] = round(cyc[1], 1)
+        if pc:
+            out["valu_per_step"] = pc.get("valu_per_step")
+            out["counters"] = pc.get("source")
+            if "cycles_per_step" in out and pc.get("valu_per_step"):
+                out["issue_frac"] = round(4.0 * pc["valu_per_step"] / out["cycles_per_step"], 4)
+        return out
 
     def _pll_redo(self) -> dict | None:
         """Diagnosis builds (-DSDR_PLL_COUNT=1) only: fraction of the PLL's 16-step chunks whose proof
@@ -362,13 +416,33 @@ class GpuStepper:
         """Host copies of the inputs and captured outputs of the checked channels."""
         sel = self.vsel.cpu().numpy()
         iq = self.iq[:, self.vsel].cpu().numpy()            # [nblocks][nv][2*block_iq]
-        return {"channels": [int(c) for c in sel], "iq": iq, "mono": self.cap_mono.cpu().numpy(),
-                "lr": self.cap_lr.cpu().numpy(), "bits": self.cap_bits.cpu().numpy(),
-                "nbits": self.cap_nbits.cpu().numpy()}
+        lr, bits = self.cap_lr.cpu().numpy(), self.cap_bits.cpu().numpy()
+        return {"channels": [int(c) for c in sel], "first_channel": self.first, "iq": iq,
+                "mono": self.cap_mono.cpu().numpy(), "lr": lr, "bits": bits, "nbits": self.cap_nbits.cpu().numpy(),
+                "digest": _digest(lr, bits)}
 
     def close(self) -> None:
         self.pipe.close()
         destroy_masked_streams(self.torch, self.pkg, self.dev, self.created)
+
+
+def _digest(lr, bits) -> str:
+    """SHA-256 over captured stereo audio and RDS bit rows ([blocks][channels][...])."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(lr).tobytes())
+    h.update(np.ascontiguousarray(bits).tobytes())
+    return h.hexdigest()
+
+
+def _pll_counters() -> dict | None:
+    """Committed SQ counters of the PLL kernel (profiles/pll_counters.json, from a rocprofv3 --pmc
+    pass with per-block PLL dispatch: PMC serialises dispatches, which the persistent launch cannot
+    run under): VALU instructions and issue quad-cycles per PLL step."""
+    try:
+        return json.loads((ROOT / "profiles" / "pll_counters.json").read_text())
+    except (OSError, ValueError):
+        return None
 
 
 def _pmc_traffic(nch: int, numerics: str):
@@ -430,6 +504,27 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
         elapsed = time.perf_counter() - t0
         if world > 1:
             elapsed = max_over_ranks(torch, dist, elapsed, gdev)
+        # ---- outside the timed region: parity of the outputs (every rank checks its own captured
+        # channels against the oracle; the receiving rank checks that the rows the gather delivered
+        # from each rank are the rows that rank produced)
+        cap = st.captured() if (not args.no_cpu_baseline and hasattr(st, "captured")) else None
+        ver = verify_captured(cap, _cpu_share() if world == 1 else max(1, _cpu_share() // 2)) if cap else None
+        gathered_check = None
+        if world > 1 and cap is not None:
+            mine = {"rank": rank, "ok": (ver or {}).get("ok"), "digest": cap["digest"],
+                    "channels": [cap["first_channel"] + c for c in cap["channels"]],
+                    "mismatches": (ver or {}).get("mismatches")}
+            objs = [None] * world if rank == 0 else None
+            dist.gather_object(mine, objs, dst=0)
+            if rank == 0:
+                got = st.gathered_digests() if (bg is not None and hasattr(st, "gathered_digests")) else None
+                gathered_check = {
+                    "ranks_oracle_ok": all(o["ok"] for o in objs),
+                    "channels": {o["rank"]: o["channels"] for o in objs},
+                    "mismatches": {o["rank"]: o["mismatches"] for o in objs if o["mismatches"]} or None,
+                    "gather_rows_equal": (None if got is None else
+                                          all(got[o["rank"]] == o["digest"] for o in objs)),
+                }
         res = None
         if rank == 0:
             total_samples = world * nch * st.info.block_iq * args.steps
@@ -469,9 +564,15 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
                 res["roofline"]["copy_GBps"] = iso["hbm_copy"]["achieved"]
                 res["roofline"]["frac_of_copy"] = round(res["roofline"]["achieved"] / iso["hbm_copy"]["achieved"], 4)
                 res["roofline_fast"] = iso.get("fast")
-            res["cpu_baseline"] = (None if args.no_cpu_baseline
-                                   else cpu_baseline_leg(args, st.captured(), timing=(world == 1)))
-            res["verified"] = (res["cpu_baseline"] or {}).get("verified", {}).get("ok")
+            res["cpu_baseline"] = (None if args.no_cpu_baseline else cpu_baseline_leg(args, None, timing=(world == 1)))
+            if ver is not None:
+                res["cpu_baseline"]["verified"] = ver
+            if gathered_check is not None:
+                res["verified_ranks"] = gathered_check
+                rows_ok = gathered_check["gather_rows_equal"] if bg is not None else True
+                res["verified"] = bool(gathered_check["ranks_oracle_ok"] and rows_ok)
+            else:
+                res["verified"] = (ver or {}).get("ok")
         return res
     finally:
         if hasattr(st, "close"):
@@ -543,19 +644,70 @@ def _check_channel(job):
     return j, bad[:4]
 
 
+def _host_cpus() -> dict:
+    """What this process may run on: nproc, the affinity mask, and the cgroup CPU quota if any."""
+    out = {"nproc": os.cpu_count()}
+    try:
+        out["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        out["affinity"] = os.cpu_count()
+    quota = None
+    try:   # cgroup v2: "max 100000" or "<quota> <period>"
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    out["cgroup_cpu_quota"] = quota
+    usable = out["affinity"] or 1
+    if quota is not None:
+        usable = min(usable, int(quota))
+    out["usable"] = max(1, usable)
+    return out
+
+
+def _reference_concurrent(exe, nproc: int, nb: int, reps: int) -> tuple[float, float]:
+    """nproc concurrent `project 0 r` processes (3 threads each, the reference's topology) on distinct
+    channels, each piping reps x nb blocks; returns (MS/s aggregate, wall seconds)."""
+    synth = _synth_module()
+    distinct = min(nproc, 16)          # channel content does not change the CPU cost; 16 distinct inputs
+    blobs = [_blob(1 + i, nb) for i in range(distinct)]
+    with cf.ThreadPoolExecutor(nproc) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(lambda i: _run_reference(exe, blobs[i % distinct], reps), range(nproc)))
+        dt = time.perf_counter() - t0
+    return nproc * reps * nb * synth.BLOCK_IQ / dt / 1e6, dt
+
+
+def verify_captured(cap: dict, workers: int) -> dict:
+    """The checker: captured GPU outputs of a few channels (mono, stereo, RDS bits of every block)
+    compared bit for bit with the oracle run on the same input bytes (worker processes)."""
+    jobs = [(j, cap["iq"][:, j], cap["mono"][:, j], cap["lr"][:, j], cap["bits"][:, j], cap["nbits"][:, j])
+            for j in range(len(cap["channels"]))]
+    with cf.ProcessPoolExecutor(max(1, min(len(jobs), workers)), mp_context=mp.get_context("spawn")) as ex:
+        results = dict(ex.map(_check_channel, jobs))
+    first = cap.get("first_channel", 0)
+    bad = {first + cap["channels"][j]: v for j, v in results.items() if v}
+    return {"ok": not bad, "channels": [first + c for c in cap["channels"]], "blocks": int(cap["iq"].shape[0]),
+            "outputs": "mono int16, stereo int16, RDS bits (every block incl. warm-up), "
+                       "bit for bit against the oracle on the same input bytes",
+            "mismatches": bad or None}
+
+
 def cpu_baseline_leg(args, cap: dict | None, timing: bool = True) -> dict:
     """Rank 0 only, outside the timed region: (1) the reference's own program (oracle/_ref/project,
     built from the unmodified sources) in its 3-thread topology on one channel; (2) the same
-    program on distinct channels concurrently over the host's CPU share (floor(cores/3) processes);
-    (3) the checker: the captured GPU outputs of a few channels compared bit for bit with the
-    oracle run on the same bytes."""
+    program on distinct channels concurrently over one GPU's CPU share (floor(cores/3) processes);
+    (3) the same over every CPU this job may use on the host (floor(usable/3) processes, the node's
+    CPU figure); (4) with `cap`, the checker (verify_captured)."""
     synth = _synth_module()
     exe = ROOT / "oracle" / "_ref" / "project"
     cores = _cpu_share()
+    host = _host_cpus()
     res: dict = {"host_cpu": _cpu_model(), "nproc": os.cpu_count(), "cpu_share": cores}
     if not timing:
         # N > 1: the CPU legs are timed at N = 1 only (BASELINE's CPU comparison is per node, and the
-        # other ranks have finished); the captured outputs are still checked below
+        # other ranks have finished); the captured outputs are still checked
         res.update({"value": None, "unit": "MS/s", "cores": 0, "kind": "reference",
                     "sample": "not timed at N > 1 (see the N = 1 line)"})
     elif exe.exists():
@@ -569,16 +721,23 @@ def cpu_baseline_leg(args, cap: dict | None, timing: bool = True) -> dict:
                               f"{reps * nblk} blocks = {reps * nblk * synth.BLOCK_IQ / 1e6:.1f} M I/Q samples of "
                               f"1 channel via stdin, {dt:.2f} s wall"})
         nproc = max(1, cores // 3)
-        nb2, reps2 = 8, 400                  # per process: 3200 blocks of its own channel
-        blobs = [_blob(1 + i, nb2) for i in range(nproc)]
-        with cf.ThreadPoolExecutor(nproc) as ex:
-            t0 = time.perf_counter()
-            list(ex.map(lambda bl: _run_reference(exe, bl, reps2), blobs))
-            dt2 = time.perf_counter() - t0
-        res["all_cores"] = {"value": round(nproc * reps2 * nb2 * synth.BLOCK_IQ / dt2 / 1e6, 3), "unit": "MS/s",
-                            "cores": 3 * nproc, "kind": "reference",
+        v, dt2 = _reference_concurrent(exe, nproc, 8, 400)     # per process: 3200 blocks of its own channel
+        res["all_cores"] = {"value": round(v, 3), "unit": "MS/s", "cores": 3 * nproc, "kind": "reference",
                             "sample": f"{nproc} concurrent `project 0 r` processes x 3 threads, distinct channels, "
-                                      f"{reps2 * nb2} blocks each, {dt2:.2f} s wall"}
+                                      f"3200 blocks each, {dt2:.2f} s wall (one GPU's CPU share)"}
+        res["host_cpus"] = host
+        # the whole host (floor(usable / 3) processes) only on request: a GPU job on this pool owns a
+        # 16-CPU share of the node, the other GPUs' jobs share the rest (SDR_BENCH_CPU_CORES)
+        if os.environ.get("SDR_BENCH_HOST_LEG", "0") == "1":
+            nproc_h = max(1, host["usable"] // 3)
+            v, dt3 = _reference_concurrent(exe, nproc_h, 8, 200)   # 1600 blocks per process
+            res["all_host_cores"] = {
+                "value": round(v, 3), "unit": "MS/s", "cores": 3 * nproc_h, "kind": "reference",
+                "processes": nproc_h, "nproc": host["nproc"], "affinity": host["affinity"],
+                "cgroup_cpu_quota": host["cgroup_cpu_quota"],
+                "sample": f"{nproc_h} concurrent `project 0 r` processes x 3 threads (floor(usable CPUs / 3); "
+                          f"usable = min(affinity {host['affinity']}, cgroup quota {host['cgroup_cpu_quota']}) "
+                          f"of nproc {host['nproc']}), 1600 blocks each, {dt3:.2f} s wall"}
     else:
         # the C restatement, one core, full pipeline (this tree built without /root/reference)
         sys.path.insert(0, str(ROOT / "oracle"))
@@ -596,15 +755,7 @@ def cpu_baseline_leg(args, cap: dict | None, timing: bool = True) -> dict:
         res.update({"value": round(n * synth.BLOCK_IQ / dt / 1e6, 3), "unit": "MS/s", "cores": 1, "kind": "port",
                     "sample": f"oracle C restatement, 1 channel x {n} blocks, 1 thread, {dt:.2f} s"})
     if cap is not None:
-        jobs = [(j, cap["iq"][:, j], cap["mono"][:, j], cap["lr"][:, j], cap["bits"][:, j], cap["nbits"][:, j])
-                for j in range(len(cap["channels"]))]
-        with cf.ProcessPoolExecutor(min(len(jobs), cores), mp_context=mp.get_context("spawn")) as ex:
-            results = dict(ex.map(_check_channel, jobs))
-        bad = {cap["channels"][j]: v for j, v in results.items() if v}
-        res["verified"] = {"ok": not bad, "channels": cap["channels"], "blocks": int(cap["iq"].shape[0]),
-                           "outputs": "mono int16, stereo int16, RDS bits (every block incl. warm-up), "
-                                      "bit for bit against the oracle on the same input bytes",
-                           "mismatches": bad or None}
+        res["verified"] = verify_captured(cap, cores)
     return res
 
 

@@ -154,11 +154,19 @@ int sdr_plls(sdr_ctx *ctx, void *stream);
  * from the device clock: its last wave's end minus the later of its signal and the previous
  * block's end) and synchronises `stream`. While a launch still waits for blocks, nothing may
  * synchronise with the PLL stream implicitly: a CU-masked stream is a blocking stream, so work on
- * the legacy null stream would wait for it (until the 5 s bound). Not with SDR_FLAG_PLL_LIBM. */
+ * the legacy null stream would wait for it (until the 5 s bound). Each block must be waited for
+ * (sdr_plls_wait) before the 16th block after it is signalled. The PLL stream must own its hardware
+ * queue (a CU-masked stream does): a kernel queued behind the waiting launch would never run.
+ * Launching again while blocks of the previous launch were never signalled first lets that launch
+ * time out and drain. Not with SDR_FLAG_PLL_LIBM. */
 int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
 int sdr_plls_signal(sdr_ctx *ctx, void *stream);
 int sdr_plls_wait(sdr_ctx *ctx, void *stream);
 int sdr_plls_report(sdr_ctx *ctx, double *block_ms, int max_blocks, int *nblocks, void *stream);
+/* Per-step cost of the last persistent launch from the waves' own clocks: shader cycles per PLL step
+ * and wave (s_memtime over each wave's compute of each block, averaged) and the shader clock over
+ * the same intervals (against the 100 MHz s_memrealtime); synchronises `stream`. */
+int sdr_plls_cycles(sdr_ctx *ctx, double *cycles_per_step, double *clock_mhz, void *stream);
 /* rds symbol/bit recovery (rds.cpp:135-167): per channel, for blocks with block_count > 5 and
  * rds_on: offset = cdr(), symbols (0/1 bytes), bits (decoded 0/1 bytes). nbits[ch] = -1 on
  * blocks that do not decode. Any output pointer may be NULL. Strides in elements. */

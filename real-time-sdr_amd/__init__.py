@@ -91,6 +91,7 @@ def lib() -> C.CDLL:
         "sdr_plls_signal": ([vp, vp], i32),
         "sdr_plls_wait": ([vp, vp], i32),
         "sdr_plls_report": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32), vp], i32),
+        "sdr_plls_cycles": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), vp], i32),
         "sdr_rds_post": ([vp, vp, sz, vp], i32),
         "sdr_ctx_buffer": ([vp, C.c_char_p, C.POINTER(vp), C.POINTER(sz), C.POINTER(i32)], i32),
         "sdr_hbm_copy": ([vp, vp, sz, vp], i32),
@@ -331,6 +332,12 @@ class Pipeline:
         n = C.c_int(0)
         check(lib().sdr_plls_report(self._h, arr, max_blocks, C.byref(n), _stream(stream)), "sdr_plls_report")
         return list(arr[:n.value])
+
+    def plls_cycles(self, stream=None) -> tuple[float, float]:
+        """(shader cycles per PLL step and wave, shader clock MHz) of the last persistent launch."""
+        cyc, mhz = C.c_double(0.0), C.c_double(0.0)
+        check(lib().sdr_plls_cycles(self._h, C.byref(cyc), C.byref(mhz), _stream(stream)), "sdr_plls_cycles")
+        return cyc.value, mhz.value
 
     def rds_post(self, out=None, bits=True, stream=None):
         check(lib().sdr_rds_post(self._h, _ptr(out), _row_stride(out) if out is not None else 0, _stream(stream)),

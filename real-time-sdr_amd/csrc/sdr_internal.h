@@ -111,12 +111,20 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
 int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
                size_t t_stride, double* rxbuf, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale,
                float phaseAdjust, float bw, hipStream_t s);
-// persistent PLLs: words = [pre_flag, done_count, err]; returns the number of waves in *waves
+// persistent PLLs: words = [pre_flag, err, (pad), (pad), done ring of PLL_DONE_RING per-sequence
+// counters]; returns the number of waves in *waves. Block sequence s is done when its ring slot
+// done[s % PLL_DONE_RING] reaches waves * (s / PLL_DONE_RING + 1): per-block counters, because
+// waves drift apart by more than a block (a wave that redoes many chunks lags the others, which
+// may already finish the next block) and one shared count would release a block early.
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
-                     unsigned long long* t0, unsigned long long* t1, uint32_t* waves, hipStream_t s);
+                     unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
+                     hipStream_t s);
 int launch_flag_store(uint32_t* flag, uint32_t v, hipStream_t s);
 int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStream_t s);
 int diag_pll_counts(unsigned long long* out, int reset);
+constexpr int PLL_WORDS_DONE = 4;      // index of the done ring in the words array
+constexpr uint32_t PLL_DONE_RING = 16; // waves stay within a few blocks of each other
+constexpr int PLL_WORDS = PLL_WORDS_DONE + (int)PLL_DONE_RING;
 
 }  // namespace sdrk
 
@@ -167,13 +175,15 @@ struct sdr_ctx {
     long long block = -1;                               // index of the current block
     long long stereo_done = -1, rds_dsp_done = -1, rds_bits_done = -1, mono_done = -1;
     long long st_pre_done = -1, st_pll_done = -1, rds_pre_done = -1, rds_pll_done = -1;
-    // persistent PLLs (sdr_plls_launch / _signal / _wait): device words [pre_flag, done_count,
-    // err], per-block timestamps of the last launch, and the host's sequence bookkeeping
+    // persistent PLLs (sdr_plls_launch / _signal / _wait): device words (launch_pll_multi), per-block
+    // timestamps of the last launch, and the host's sequence bookkeeping
     uint32_t* pers_words = nullptr;
     unsigned long long *pers_t0 = nullptr, *pers_t1 = nullptr;
+    unsigned long long* pers_cyc = nullptr;             // [block][2]: sums over waves of cycles, 100 MHz ticks
     int pers_tcap = 0, pers_last_n = 0;
     uint32_t pers_launched = 0, pers_signaled = 0, pers_waves = 0;
     uint32_t pers_base = 0;                             // sequence number of the last launch's first block
+    uint32_t pers_waited = 0;                           // sequence numbers below this have been waited for
     long long pers_first_block = -1;                    // the context block that sequence number belongs to
     hipStream_t pers_stream = nullptr;                  // stream of the last launch
     long long pers_block = -1;                          // block of the last signal

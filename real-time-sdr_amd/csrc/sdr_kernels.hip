@@ -1317,33 +1317,37 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
         // bounded wait (PLL_WAIT_TICKS) and still count them done. Let it drain, then resynchronise
         // the host's sequence numbers with the device words so this launch starts clean.
         HIP_TRY(hipStreamSynchronize(c->pers_stream));
-        c->pers_signaled = c->pers_launched;
+        c->pers_signaled = c->pers_waited = c->pers_launched;
         HIP_TRY(hipMemcpyAsync(c->pers_words, &c->pers_launched, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     }
     if (!c->pers_words) {
         void* w = nullptr;
-        HIP_TRY(hipMalloc(&w, 4 * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&w, PLL_WORDS * sizeof(uint32_t)));
         c->allocs.push_back(w);
         c->pers_words = static_cast<uint32_t*>(w);
-        HIP_TRY(hipMemsetAsync(c->pers_words, 0, 4 * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(c->pers_words, 0, PLL_WORDS * sizeof(uint32_t), s));
     }
     if (c->pers_tcap < nblocks) {
         // timestamp arrays: allocated once with room for long phases (a later, longer launch
         // grows them here, outside any timed loop that reuses the capacity)
         const int cap = std::max(nblocks, 4096);
         if (c->pers_tcap > 0) HIP_TRY(hipStreamSynchronize(c->pers_stream));   // the last launch still writes them
-        void *a = nullptr, *b = nullptr;
+        void *a = nullptr, *b = nullptr, *cy = nullptr;
         HIP_TRY(hipMalloc(&a, (size_t)cap * sizeof(unsigned long long)));
         c->allocs.push_back(a);
         HIP_TRY(hipMalloc(&b, (size_t)cap * sizeof(unsigned long long)));
         c->allocs.push_back(b);
+        HIP_TRY(hipMalloc(&cy, (size_t)cap * 2 * sizeof(unsigned long long)));
+        c->allocs.push_back(cy);
         c->pers_t0 = static_cast<unsigned long long*>(a);
         c->pers_t1 = static_cast<unsigned long long*>(b);
+        c->pers_cyc = static_cast<unsigned long long*>(cy);
         c->pers_tcap = cap;
     }
     HIP_TRY(hipMemsetAsync(c->pers_t0, 0xFF, (size_t)nblocks * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(c->pers_t1, 0, (size_t)nblocks * sizeof(unsigned long long), s));
-    HIP_TRY(hipMemsetAsync(c->pers_words + 2, 0, sizeof(uint32_t), s));   // err of this launch
+    HIP_TRY(hipMemsetAsync(c->pers_cyc, 0, (size_t)nblocks * 2 * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(c->pers_words + 1, 0, sizeof(uint32_t), s));   // err of this launch
     const int n = c->info.block_if, nch = c->nch;
     PllJobs2 jobs{};
     const int first_parity = c->parity ^ 1;   // the parity the next sdr_frontend switches to: p[0]
@@ -1356,7 +1360,7 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     }
     uint32_t waves = 0;
     const int r = launch_pll_multi(jobs, n, nch, nblocks, c->pers_words, c->pers_launched, c->pers_t0, c->pers_t1,
-                                   &waves, s);
+                                   c->pers_cyc, &waves, s);
     if (r) return r;
     c->pers_waves = waves;
     c->pers_base = c->pers_launched;
@@ -1380,6 +1384,11 @@ int sdr_plls_signal(sdr_ctx* c, void* stream) {
     if (c->block != want_block)
         return fail(SDR_E_INVALID, "plls_signal: block %lld, but the launch expects block %lld next", c->block,
                     want_block);
+    // a block's done slot is reused PLL_DONE_RING sequence numbers later: every block must have been
+    // waited for (sdr_plls_wait) before the one that reuses its slot is signalled
+    if (c->pers_signaled - c->pers_waited >= PLL_DONE_RING)
+        return fail(SDR_E_INVALID, "plls_signal: %u blocks signalled but not waited for (at most %u in flight)",
+                    c->pers_signaled - c->pers_waited, PLL_DONE_RING);
     const int r = launch_flag_store(c->pers_words, c->pers_signaled + 1u, S(stream));
     if (r) return r;
     c->pers_block = c->block;
@@ -1392,8 +1401,11 @@ int sdr_plls_signal(sdr_ctx* c, void* stream) {
 int sdr_plls_wait(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (c->pers_block != c->block) return fail(SDR_E_INVALID, "plls_wait: sdr_plls_signal this block first");
-    const uint32_t want = c->pers_waves * (c->pers_block_seq + 1u);
-    return launch_flag_wait(c->pers_words + 1, want, c->pers_words + 2, S(stream));
+    // every wave has finished this block's sequence number (its slot of the done ring)
+    const uint32_t seq = c->pers_block_seq;
+    const uint32_t want = c->pers_waves * (seq / PLL_DONE_RING + 1u);
+    if ((int32_t)(seq + 1u - c->pers_waited) > 0) c->pers_waited = seq + 1u;
+    return launch_flag_wait(c->pers_words + PLL_WORDS_DONE + seq % PLL_DONE_RING, want, c->pers_words + 1, S(stream));
 }
 
 int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, void* stream) {
@@ -1401,7 +1413,7 @@ int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, 
     hipStream_t s = S(stream);
     const int n = std::min(c->pers_last_n, std::max(max_blocks, 0));
     std::vector<unsigned long long> t0((size_t)std::max(n, 1)), t1((size_t)std::max(n, 1));
-    uint32_t words[4] = {0, 0, 0, 0};
+    uint32_t words[PLL_WORDS] = {};
     HIP_TRY(hipMemcpyAsync(words, c->pers_words, sizeof(words), hipMemcpyDeviceToHost, s));
     if (n > 0) {
         HIP_TRY(hipMemcpyAsync(t0.data(), c->pers_t0, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -1416,10 +1428,28 @@ int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, 
         block_ms[j] = (t1[j] >= from) ? (double)(t1[j] - from) * 1e-5 : -1.0;
     }
     if (nblocks) *nblocks = n;
-    if (words[2])
+    if (words[1])
         return fail(SDR_E_HIP, "plls_report: a persistent PLL wait timed out (outputs invalid): err %u, flag %u, "
-                    "done %u, signalled %u, launched %u, waves %u", words[2], words[0], words[1], c->pers_signaled,
-                    c->pers_launched, c->pers_waves);
+                    "signalled %u, launched %u, waves %u", words[1], words[0], c->pers_signaled, c->pers_launched,
+                    c->pers_waves);
+    return SDR_OK;
+}
+
+int sdr_plls_cycles(sdr_ctx* c, double* cycles_per_step, double* clock_mhz, void* stream) {
+    if (!c || !c->pers_cyc || c->pers_last_n <= 0) return fail(SDR_E_INVALID, "plls_cycles: no persistent launch");
+    hipStream_t s = S(stream);
+    const int n = c->pers_last_n;
+    std::vector<unsigned long long> v((size_t)2 * n);
+    HIP_TRY(hipMemcpyAsync(v.data(), c->pers_cyc, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    double cyc = 0.0, ticks = 0.0;
+    for (int j = 0; j < n; j++) {
+        cyc += (double)v[2 * j];
+        ticks += (double)v[2 * j + 1];
+    }
+    const double steps = (double)c->pers_waves * n * c->info.block_if;
+    if (cycles_per_step) *cycles_per_step = steps > 0 ? cyc / steps : -1.0;
+    if (clock_mhz) *clock_mhz = ticks > 0 ? cyc / ticks * 100.0 : -1.0;   // s_memrealtime runs at 100 MHz
     return SDR_OK;
 }
 

@@ -478,9 +478,9 @@ constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrea
 template <bool VEC>
 __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
                                                   const uint32_t* pre_flag, uint32_t pre_first,
-                                                  uint32_t* done_count, uint32_t* err,
+                                                  uint32_t* done_ring, uint32_t* err,
                                                   unsigned long long* t_start, unsigned long long* t_end,
-                                                  int sys_acquire) {
+                                                  unsigned long long* t_cyc, int sys_acquire) {
     extern __shared__ double wtab[];
     const int ch = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = ch < nch;
@@ -502,10 +502,12 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
             }
             if (dead && threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        unsigned long long c0 = 0, r0 = 0;   // this wave's shader-clock and 100 MHz stamps of the block
         if (!dead) {
+            c0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
             if (threadIdx.x == 0)
-                __hip_atomic_fetch_min(t_start + j, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_min(t_start + j, r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const double toff0 = active ? jb.st[ch].trigOffset : 0.0;
             const double w = 2 * 3.14159265358979323846 * (jb.freq / jb.Fs);
             const double toff_l0 = __shfl(toff0, 0);
@@ -522,10 +524,16 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
             __syncthreads();   // every lane's table reads and state/phase stores issued before the release
         }
         if (threadIdx.x == 0) {
-            if (!dead)
-                __hip_atomic_fetch_max(t_end + j, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(done_count, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (!dead) {
+                const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+                __hip_atomic_fetch_max(t_end + j, r1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // sums over waves: shader cycles and 100 MHz ticks spent on block j (sdr_plls_cycles)
+                __hip_atomic_fetch_add(t_cyc + 2 * j, c1 - c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(t_cyc + 2 * j + 1, r1 - r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // block sequence pre_first + j done by this wave: its own slot of the ring
+            __hip_atomic_fetch_add(done_ring + (pre_first + (uint32_t)j) % PLL_DONE_RING, 1u, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -701,7 +709,8 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
 }
 
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
-                     unsigned long long* t0, unsigned long long* t1, uint32_t* waves, hipStream_t s) {
+                     unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
+                     hipStream_t s) {
     bool vec = true;
     for (int k = 0; k < 2; k++)
         for (int q = 0; q < 2; q++) {
@@ -718,10 +727,10 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
     const int sys_acq = (acq && std::strcmp(acq, "system") == 0) ? 1 : 0;
     if (vec)
         hipLaunchKernelGGL(k_pll_multi<true>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
-                           words, pre_first, words + 1, words + 2, t0, t1, sys_acq);
+                           words, pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc, sys_acq);
     else
         hipLaunchKernelGGL(k_pll_multi<false>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
-                           words, pre_first, words + 1, words + 2, t0, t1, sys_acq);
+                           words, pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc, sys_acq);
     LAUNCH_CHECK();
     return SDR_OK;
 }

@@ -27,6 +27,10 @@ class BlockGather:
         self.torch, self.dist, self.world, self.dst = torch, dist, world, dst
         self.rank = dist.get_rank()
         self.shapes = {k: (tuple(s), dt) for k, (s, dt) in shapes.items()}
+        # gloo moves host tensors only: device rows are staged through host memory (a blocking copy
+        # on the current stream; the GPU rank path uses RCCL, where rows stay on the device)
+        self.host_staged = dist.get_backend() == "gloo" and torch.device(device).type != "cpu"
+        buf_dev = "cpu" if self.host_staged else device
         self.out = {}
         self.row_bytes = {}
         for k, (s, dt) in self.shapes.items():
@@ -35,7 +39,7 @@ class BlockGather:
                 rb *= d
             self.row_bytes[k] = rb
             if self.rank == dst:
-                self.out[k] = [torch.empty((s[0], rb), dtype=torch.uint8, device=device) for _ in range(world)]
+                self.out[k] = [torch.empty((s[0], rb), dtype=torch.uint8, device=buf_dev) for _ in range(world)]
         self.steps = 0
 
     def gather(self, **tensors) -> dict | None:
@@ -46,6 +50,8 @@ class BlockGather:
             if tuple(t.shape) != shape or t.dtype != dt:
                 raise ValueError(f"{k}: expected {shape} {dt}, got {tuple(t.shape)} {t.dtype}")
             src = t.contiguous().view(shape[0], -1).view(self.torch.uint8)
+            if self.host_staged:
+                src = src.cpu()
             parts = self.out.get(k) if self.rank == self.dst else None
             self.dist.gather(src, parts, dst=self.dst)
             if parts is not None:
@@ -62,6 +68,8 @@ class BlockGather:
 
 def max_over_ranks(torch, dist, seconds: float, device) -> float:
     """The job's time is the slowest rank's (bench contract: max over ranks)."""
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -370,7 +370,7 @@ def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda):
     nch, nb = 8, 3
     iqs = [channel_input(synth, 500 + c, nb) for c in range(nch)]
     d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
-    ref = _run_pipeline(pkg, torch, iqs, nb - 1)
+    ref = _run_pipeline(pkg, torch, iqs, nb)
     pipe = pkg.Pipeline(nch)
     s_pll, s_post = torch.cuda.Stream(), torch.cuda.Stream()
     pipe.plls_launch(nb, stream=s_pll)
@@ -387,6 +387,58 @@ def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda):
         assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
     with pytest.raises(pkg.SdrError, match="timed out"):
         pipe.plls_report(stream=s_pll)
+    # the context recovers: the abandoned block's PLL never ran (its state is still block 1's), a
+    # new launch resynchronises the sequence numbers and clears the error word, and block 2 then
+    # comes out as in the one-stream pipeline
+    pipe.plls_launch(1, stream=s_pll)
+    pipe.frontend(d[nb - 1])
+    pipe.stereo_pre()
+    pipe.rds_pre()
+    pipe.plls_signal()
+    pipe.plls_wait(stream=s_post)
+    pipe.stereo_post(lr, stream=s_post)
+    pipe.rds_post(None, bits=False, stream=s_post)
+    s_post.synchronize()
+    assert np.array_equal(lr.cpu().numpy(), ref["stereo"][nb - 1]), "stereo after recovery"
+    assert len(pipe.plls_report(stream=s_pll)) == 1
+    pipe.close()
+
+
+def test_persistent_plls_signal_checks_block_order(pkg, synth, torch_cuda):
+    """A launch fixes each block's buffer parity from the block that follows it: signalling a block
+    the launch does not cover next (here: the block that was already produced when the launch was
+    made) is rejected; the blocks that do follow it run and match the one-stream pipeline."""
+    torch = torch_cuda
+    nch, nb = 4, 3
+    iqs = [channel_input(synth, 600 + c, nb) for c in range(nch)]
+    d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
+    ref = _run_pipeline(pkg, torch, iqs, nb)
+    pipe = pkg.Pipeline(nch)
+    s_pll, s_post = torch.cuda.Stream(), torch.cuda.Stream()
+    lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
+    pipe.frontend(d[0])
+    pipe.plls_launch(nb - 1, stream=s_pll)       # covers blocks 1 and 2
+    pipe.stereo_pre()
+    pipe.rds_pre()
+    with pytest.raises(pkg.SdrError, match="expects block 1"):
+        pipe.plls_signal()
+    pipe.stereo_pll()                            # block 0 the ordinary way
+    pipe.rds_pll()
+    pipe.stereo_post(lr)
+    pipe.rds_post(None, bits=False)
+    torch.cuda.current_stream().synchronize()
+    assert np.array_equal(lr.cpu().numpy(), ref["stereo"][0])
+    for b in range(1, nb):
+        pipe.frontend(d[b])
+        pipe.stereo_pre()
+        pipe.rds_pre()
+        pipe.plls_signal()
+        pipe.plls_wait(stream=s_post)
+        pipe.stereo_post(lr, stream=s_post)
+        pipe.rds_post(None, bits=False, stream=s_post)
+        s_post.synchronize()
+        assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
+    assert len(pipe.plls_report(stream=s_pll)) == nb - 1
     pipe.close()
 
 
