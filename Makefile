@@ -32,6 +32,9 @@ lib: $(LIB)
 host: $(HOSTLIB) $(CLI) $(MULTI)
 
 # one object per translation unit (compiled in parallel), linked into the shared library
+# the stage kernels keep their f32 multiply-adds scalar (packed f32 runs at half rate): no SLP
+build/sdr_kernels.hip.o: HIPFLAGS += -fno-slp-vectorize
+
 build/%.o: $(PKG)/csrc/% $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<

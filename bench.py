@@ -229,8 +229,7 @@ class GpuStepper:
         pipe.mono(self.mono, stream=s_fe)                     # mono.cpp:34-42
         with torch.cuda.stream(s_fe):
             torch.index_select(self.mono, 0, self.vsel, out=self.cap_mono[b])
-        pipe.stereo_pre(stream=s_fe)                          # stereo.cpp:74, :80
-        pipe.rds_pre(stream=s_fe)                             # rds.cpp:105-116
+        pipe.pre(stream=s_fe)                                 # stereo.cpp:74, :80 + rds.cpp:105-116
         if self.persist:                                      # stereo.cpp:77 + rds.cpp:119
             pipe.plls_signal(stream=s_fe)
             pipe.plls_wait(stream=s_post)

@@ -36,6 +36,9 @@ extern "C" {
 /* Context flags */
 #define SDR_FLAG_FAST_FRONTEND 0x1  /* FMA front end: fm_demod within 1e-6 rel., not bit-exact */
 #define SDR_FLAG_PLL_LIBM 0x2       /* PLL via per-step f64 libm calls (A/B reference; env SDR_PLL=libm) */
+#define SDR_FLAG_KEEP_INTERMEDIATES 0x4  /* post stages store every intermediate row (carrier, stereo_dc,
+                                          * ipll) for sdr_ctx_buffer; by default the NCO, mixers and
+                                          * resamplers are fused and only the rows' history is stored */
 
 /* pllblock_args, include/pll.h:10-17 (same field order and types) */
 typedef struct sdr_pll_state {
@@ -139,6 +142,10 @@ int sdr_stereo_pre(sdr_ctx *ctx, void *stream);
 int sdr_stereo_pll(sdr_ctx *ctx, void *stream);
 int sdr_stereo_post(sdr_ctx *ctx, int16_t *lr, size_t lr_stride, void *stream);
 int sdr_rds_pre(sdr_ctx *ctx, void *stream);
+/* sdr_stereo_pre + sdr_rds_pre of the current block on ONE stream: the pilot, band and RDS band
+ * BPFs read the staged fm_demod window once (stereo.cpp:74,80 and rds.cpp:105 share the input),
+ * then the squared-RDS BPF. For callers that run both pre parts on the same stream. */
+int sdr_pre(sdr_ctx *ctx, void *stream);
 int sdr_rds_pll(sdr_ctx *ctx, void *stream);
 int sdr_rds_post(sdr_ctx *ctx, float *rds_clean, size_t rds_stride, void *stream);
 /* stereo_pll + rds_pll of the current block in one dispatch (2 x nch independent recurrences);
@@ -179,7 +186,8 @@ int sdr_push_fm_demod(sdr_ctx *ctx, const float *fm, size_t fm_stride, void *str
 /* Copy out the context's current-block fm_demod [nch][block_if] (the reference's queue payload) */
 int sdr_get_fm_demod(sdr_ctx *ctx, float *fm, size_t fm_stride, void *stream);
 /* Debug / parity access to intermediates of the current block (device pointers into the
- * context, valid until the next sdr_frontend): name in {"fm","pilot","carrier","band","rds_band",
+ * context, valid until the next sdr_frontend; "carrier", "stereo_dc" and "ipll" hold whole rows only
+ * with SDR_FLAG_KEEP_INTERMEDIATES): name in {"fm","pilot","carrier","band","rds_band",
  * "gen_pilot","ipll","rds_dc","rds_filt","rds_clean","stereo_dc"}; *stride in elements. */
 int sdr_ctx_buffer(sdr_ctx *ctx, const char *name, const float **ptr, size_t *stride, int *len);
 

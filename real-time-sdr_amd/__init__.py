@@ -28,6 +28,7 @@ SDR_MAX_SYMS = 256
 SDR_MAX_BITS = 256
 FLAG_FAST_FRONTEND = 0x1
 FLAG_PLL_LIBM = 0x2
+FLAG_KEEP_INTERMEDIATES = 0x4
 
 _lib = None
 
@@ -85,6 +86,7 @@ def lib() -> C.CDLL:
         "sdr_stereo_pll": ([vp, vp], i32),
         "sdr_stereo_post": ([vp, vp, sz, vp], i32),
         "sdr_rds_pre": ([vp, vp], i32),
+        "sdr_pre": ([vp, vp], i32),
         "sdr_rds_pll": ([vp, vp], i32),
         "sdr_plls": ([vp, vp], i32),
         "sdr_plls_launch": ([vp, i32, vp], i32),
@@ -308,6 +310,10 @@ class Pipeline:
 
     def rds_pre(self, stream=None):
         check(lib().sdr_rds_pre(self._h, _stream(stream)), "sdr_rds_pre")
+
+    def pre(self, stream=None):
+        """stereo_pre + rds_pre on one stream, the three fm_demod BPFs sharing one staged window."""
+        check(lib().sdr_pre(self._h, _stream(stream)), "sdr_pre")
 
     def rds_pll(self, stream=None):
         check(lib().sdr_rds_pll(self._h, _stream(stream)), "sdr_rds_pll")

@@ -31,6 +31,7 @@
 
 #include "sdr_amd.h"
 #include "pll_math.h"
+#include "nco.h"
 
 #pragma clang fp contract(off)
 
@@ -117,21 +118,35 @@ __global__ __launch_bounds__(BLK) void k_fir(const float* __restrict__ x, size_t
 // The IF-rate 101-tap FIRs without decimation (filter.cpp:106-121 with D = 1: pilot/band BPFs
 // stereo.cpp:74,80, RDS BPF rds.cpp:105, squared-RDS BPF :116, RRC :133), register-blocked:
 // each thread computes FRB_R consecutive outputs from a window of FRB_R + 100 samples read once
-// from LDS (16-byte reads), the taps are wave-uniform scalar loads, and every output still sums
-// h[k] * x[n-k] in ascending k as an f32 product then an f32 add (no contraction). NT = 2: two tap
-// sets over one window (the stereo pilot and band filters).
+// from LDS (16-byte reads), and every output still sums h[k] * x[n-k] in ascending k as an f32
+// product then an f32 add (no contraction). NT tap sets (1..3) share one staged window: the stereo
+// pilot and band filters and the RDS band filter all read fm_demod (stereo.cpp:74,80, rds.cpp:105).
+// Taps are wave-uniform scalar operands, fetched FRB_TC at a time: scalar loads return out of
+// order, so every wait for one is lgkmcnt(0); the next chunk is therefore requested only after the
+// current chunk's first products have waited for it, and its latency hides behind the rest of the
+// chunk (FRB_TC x R x NT multiply-adds) instead of stalling every tap.
 // ------------------------------------------------------------------------------------------
 constexpr int FRB_T = 101;                 // taps (rf_taps, project.cpp:61)
 constexpr int FRB_R = 8;                   // outputs per thread
 constexpr int FRB_TILE = BLK * FRB_R;      // outputs per workgroup
 constexpr int FRB_W = FRB_TILE + FRB_T - 1 + 3;   // staged samples (+3: whole 16-byte reads)
 
+// Up to three tap sets over one input window. Output t goes to y[t] (stride y_stride[t]); y[0] may
+// also get its PLL reciprocals (rx0), and y[2] the history of an extended stream (hist2_src: the
+// other parity's row, copied in front by the first tile of each channel).
+struct FirRb {
+    const float* h[3];
+    float* y[3];
+    size_t y_stride[3];
+    double* rx0;
+    size_t rx_stride;
+    const float* hist2_src;
+};
+
 template <int NT, bool SQUARE>
 __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, size_t x_stride,
-                                                const float* __restrict__ hist, size_t hist_stride,
-                                                const float* __restrict__ h0, const float* __restrict__ h1, int ny,
-                                                float* __restrict__ y0, float* __restrict__ y1, size_t y_stride,
-                                                double* __restrict__ rx0, size_t rx_stride) {
+                                                const float* __restrict__ hist, size_t hist_stride, int ny,
+                                                const FirRb f) {
     constexpr int T = FRB_T, R = FRB_R;
     __shared__ __attribute__((aligned(16))) float sx[(FRB_W + 3) & ~3];
     const int ch = blockIdx.y, tid = threadIdx.x;
@@ -155,6 +170,8 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
             if (i < W) sx[i] = SQUARE ? v[u] * v[u] : v[u];       // rds.cpp:111-113
         }
     }
+    if (NT == 3 && f.hist2_src && blockIdx.x == 0 && tid < HIST)  // y[2]'s history (extended stream)
+        f.y[2][(size_t)ch * f.y_stride[2] + tid - HIST] = f.hist2_src[(size_t)ch * f.y_stride[2] + ny - HIST + tid];
     __syncthreads();
     const int nb = n0 + tid * R;
     if (nb >= ny) return;
@@ -166,50 +183,82 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
         const float4 v = reinterpret_cast<const float4*>(sx + tid * R)[i];
         w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
-    float a0[R], a1[R];
+    float a[NT][R];
 #pragma unroll
-    for (int j = 0; j < R; j++) { a0[j] = 0.0f; a1[j] = 0.0f; }
+    for (int t = 0; t < NT; t++)
 #pragma unroll
-    for (int k = 0; k < T; k++) {
-        const float c0 = h0[k];
-        const float c1 = (NT == 2) ? h1[k] : 0.0f;
+        for (int j = 0; j < R; j++) a[t][j] = 0.0f;
+    // taps: scalar loads issued by hand (the compiler would wait for every outstanding scalar load
+    // at each tap's first use), one chunk of FRB_TC taps per tap set ahead
+    constexpr int FRB_TC = 4;
+    constexpr int FRB_NC = (FRB_T + FRB_TC - 1) / FRB_TC;   // chunks (tap buffers are padded past 101)
+    typedef float f4v __attribute__((ext_vector_type(FRB_TC)));
+    f4v buf[2][NT];                                     // chunk c in buf[c & 1]
+    // base address in an SGPR pair, byte offset in an SGPR (not one address pair per chunk)
+    auto load = [&](f4v& d, const float* hp, int c) {
+        asm volatile("s_load_dwordx4 %0, %1, %2" : "=s"(d) : "s"(hp), "s"(c * FRB_TC * 4) : "memory");
+    };
 #pragma unroll
-        for (int j = 0; j < R; j++) {
-            const float v = w[j + T - 1 - k];
-            a0[j] = a0[j] + c0 * v;                               // filter.cpp:115
-            if (NT == 2) a1[j] = a1[j] + c1 * v;
-            // keep the MACs scalar: packed f32 ops run at half rate (tools/microbench/valu_rate.hip)
-            // and pairing neighbouring outputs costs register realignment and occupancy
-            if (NT == 1 && (j & 1) == 0) asm volatile("" : "+v"(a0[j]));
-        }
-    }
-    float* o0 = y0 + (size_t)ch * y_stride + nb;
-    float* o1 = (NT == 2) ? y1 + (size_t)ch * y_stride + nb : nullptr;
-    if (nb + R <= ny) {
+    for (int t = 0; t < NT; t++) load(buf[0][t], f.h[t], 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int j = 0; j < R; j += 4) {
-            reinterpret_cast<float4*>(o0 + j)[0] = make_float4(a0[j], a0[j + 1], a0[j + 2], a0[j + 3]);
-            if (NT == 2) reinterpret_cast<float4*>(o1 + j)[0] = make_float4(a1[j], a1[j + 1], a1[j + 2], a1[j + 3]);
-        }
-    } else {
+    for (int c = 0; c < FRB_NC; c++) {
 #pragma unroll
-        for (int j = 0; j < R; j++) {
-            if (nb + j < ny) {
-                o0[j] = a0[j];
-                if (NT == 2) o1[j] = a1[j];
+        for (int kk = 0; kk < FRB_TC; kk++) {
+            const int k = c * FRB_TC + kk;
+            if (k < T) {
+#pragma unroll
+                for (int j = 0; j < R; j++) {
+                    const float v = w[j + T - 1 - k];
+#pragma unroll
+                    for (int t = 0; t < NT; t++) a[t][j] = a[t][j] + buf[c & 1][t][kk] * v;   // filter.cpp:115
+                    // the MACs stay scalar (this unit is built with -fno-slp-vectorize): packed f32 ops
+                    // run at half rate (tools/microbench/valu_rate.hip), and pairing neighbouring
+                    // outputs costs register realignment and occupancy
+                }
+            }
+            if (kk == 0 && c + 1 < FRB_NC) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = 0; t < NT; t++) load(buf[(c + 1) & 1][t], f.h[t], c + 1);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
+        if (c + 1 < FRB_NC) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // chunk c + 1 landed
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
-    if (rx0) {                                                    // y0 feeds a PLL: its reciprocal
-        double* r = rx0 + (size_t)ch * rx_stride + nb;
+    // every sum is complete here: otherwise the compiler sinks the second and third tap sets' products
+    // past the first set's (divergent) stores and spills their taps from SGPRs
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+#pragma unroll
+        for (int j = 0; j < R; j++) asm volatile("" : "+v"(a[t][j]));
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        float* o = f.y[t] + (size_t)ch * f.y_stride[t] + nb;
         if (nb + R <= ny) {
 #pragma unroll
-            for (int j = 0; j < R; j += 2)
-                reinterpret_cast<double2*>(r + j)[0] = make_double2(pllm::pll_rx(a0[j]), pllm::pll_rx(a0[j + 1]));
+            for (int j = 0; j < R; j += 4)
+                reinterpret_cast<float4*>(o + j)[0] = make_float4(a[t][j], a[t][j + 1], a[t][j + 2], a[t][j + 3]);
         } else {
 #pragma unroll
             for (int j = 0; j < R; j++)
-                if (nb + j < ny) r[j] = pllm::pll_rx(a0[j]);
+                if (nb + j < ny) o[j] = a[t][j];
+        }
+    }
+    if (f.rx0) {                                                  // y[0] feeds a PLL: its reciprocal
+        double* r = f.rx0 + (size_t)ch * f.rx_stride + nb;
+        if (nb + R <= ny) {
+#pragma unroll
+            for (int j = 0; j < R; j += 2)
+                reinterpret_cast<double2*>(r + j)[0] = make_double2(pllm::pll_rx(a[0][j]), pllm::pll_rx(a[0][j + 1]));
+        } else {
+#pragma unroll
+            for (int j = 0; j < R; j++)
+                if (nb + j < ny) r[j] = pllm::pll_rx(a[0][j]);
         }
     }
 }
@@ -301,6 +350,45 @@ constexpr int RLC_TN = 32;     // outputs per workgroup (8 per wave)
 constexpr int RLC_XL = 3;      // staged samples per lane and row: 64 * 3 >= the q span + look-back
 constexpr int RLC_HL = 2;      // staged taps per lane and polyphase row: 64 * 2 >= L4
 
+// four outputs of the 247/640 resampler whose q offsets from the first are (0, D1, D2, D3):
+// acc[k] = sum_{j<101} hr[k*L4 + j] * x[q_k - j] in ascending j, x[q_0 - 100 + i] = xr[i]
+template <int D1, int D2, int D3>
+__device__ __forceinline__ void lc_group(const float* __restrict__ xr, const float* __restrict__ hr, int L4,
+                                         float (&acc)[4]) {
+    constexpr int NW = D3 + 101;
+    constexpr int DK[4] = {0, D1, D2, D3};
+    float w[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) w[i] = xr[i];
+#pragma unroll
+    for (int k = 0; k < 4; k++) acc[k] = 0.0f;
+    // taps of the 4 rows, 4 at a time (16-byte broadcasts), one chunk ahead; the barriers keep the
+    // scheduler from hoisting every chunk's reads (4 x 104 registers) to the top
+    float4 cur[4], nxt[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cur[k] = *reinterpret_cast<const float4*>(hr + k * L4);
+#pragma unroll
+    for (int j0 = 0; j0 < 104; j0 += 4) {
+        if (j0 + 4 < 104) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) nxt[k] = *reinterpret_cast<const float4*>(hr + k * L4 + j0 + 4);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float hv[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const int j = j0 + jj;
+                if (j < 101) acc[k] = acc[k] + hv[jj] * w[DK[k] + 100 - j];     // filter.cpp:139-141
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) cur[k] = nxt[k];
+    }
+}
+
 template <int NTAP>   // > 0: every polyphase row has exactly NTAP taps (fully unrolled sums)
 __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x, size_t x_stride, int hist_lo,
                                                      const float* __restrict__ hp, const int* __restrict__ cnt,
@@ -367,6 +455,49 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
     __syncthreads();
     const int ch = c0 + lane;
     float out[PW];
+    if (NTAP == 101) {
+        // groups of 4 consecutive outputs from one register window: their q offsets (q_k - q_0) follow
+        // one of four patterns for the 247/640 ratio (the fraction of 640 n / 247 picks it), a
+        // wave-uniform branch into statically indexed code; the window is read from LDS once per
+        // group (109 samples for 4 outputs instead of 4 x 101) and each tap row as 16-byte broadcasts
+        static_assert(PW % 4 == 0, "whole groups");
+#pragma unroll
+        for (int g = 0; g < PW / 4; g++) {
+            const int o = wave * PW + 4 * g;
+            bool done = false;
+            if (o + 3 < nn) {
+                const int q0 = ptq[n0 + o] >> 8;
+                const int d1 = (ptq[n0 + o + 1] >> 8) - q0, d2 = (ptq[n0 + o + 2] >> 8) - q0,
+                          d3 = (ptq[n0 + o + 3] >> 8) - q0;
+                const float* xr = sx + lane * SW + (q0 - qlo) - 100;   // xr[i] = x[q0 - 100 + i]
+                const float* hr = sh + o * L4;
+                float acc4[4];
+                done = true;
+                if (d1 == 3 && d2 == 5 && d3 == 8) lc_group<3, 5, 8>(xr, hr, L4, acc4);
+                else if (d1 == 2 && d2 == 5 && d3 == 7) lc_group<2, 5, 7>(xr, hr, L4, acc4);
+                else if (d1 == 2 && d2 == 5 && d3 == 8) lc_group<2, 5, 8>(xr, hr, L4, acc4);
+                else if (d1 == 3 && d2 == 6 && d3 == 8) lc_group<3, 6, 8>(xr, hr, L4, acc4);
+                else done = false;
+                if (done) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) out[4 * g + k] = acc4[k];
+                }
+            }
+            if (!done) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    float acc = 0.0f;
+                    if (o + k < nn) {
+                        const int e = ptq[n0 + o + k];
+                        const float* xr = sx + lane * SW + ((e >> 8) - qlo);
+                        const float* hr = sh + (o + k) * L4;
+                        for (int j = 0; j < 101; j++) acc = acc + hr[j] * xr[-j];
+                    }
+                    out[4 * g + k] = acc;
+                }
+            }
+        }
+    } else
 #pragma unroll
     for (int o8 = 0; o8 < PW; o8++) {
         const int o = wave * PW + o8;
@@ -409,6 +540,244 @@ int resample_lc_span(int L, int U, int D) {   // samples a tile reads: q span + 
 size_t resample_lc_lds_bytes(int L, int U, int D) {
     const int W = resample_lc_span(L, U, D);
     return (size_t)((((64 * (W | 1)) + 3) & ~3) + RLC_TN * ((L + 3) & ~3)) * sizeof(float);
+}
+
+// ------------------------------------------------------------------------------------------
+// Audio resamplers with U == 1 (mode 0: D = 5, mode 1: D = 9; filter.cpp:123-147 with one
+// polyphase row of 101 taps), register-blocked: a thread computes AR consecutive outputs from a
+// window of D*(AR-1) + 101 samples read once from LDS, the taps are scalar operands fetched in
+// chunks of 4 by hand-issued scalar loads (as k_fir_rb), and every output sums h[j] * x[nD - j] in
+// ascending j as an f32 product then an f32 add.
+// ------------------------------------------------------------------------------------------
+constexpr int AR = 4;                       // audio outputs per thread
+constexpr int AT = 128;                     // threads per workgroup
+constexpr int ATILE = AR * AT;              // audio outputs per workgroup
+
+// acc[r] = sum_{j<101} h[j] * w[D*r + 100 - j] (ascending j), h wave-uniform
+template <int D, int NW>
+__device__ __forceinline__ void audio_mac(const float* __restrict__ h, const float (&w)[NW], float (&acc)[AR]) {
+    constexpr int T = 101, TC = 4, NC = (T + TC - 1) / TC;   // tap buffers are padded past 101
+    typedef float f4v __attribute__((ext_vector_type(TC)));
+    f4v buf[2];
+    auto load = [&](f4v& d, int c) {
+        asm volatile("s_load_dwordx4 %0, %1, %2" : "=s"(d) : "s"(h), "s"(c * TC * 4) : "memory");
+    };
+#pragma unroll
+    for (int r = 0; r < AR; r++) acc[r] = 0.0f;
+    load(buf[0], 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+#pragma unroll
+        for (int kk = 0; kk < TC; kk++) {
+            const int j = c * TC + kk;
+            if (j < T) {
+#pragma unroll
+                for (int r = 0; r < AR; r++) acc[r] = acc[r] + buf[c & 1][kk] * w[D * r + T - 1 - j];
+            }
+            if (kk == 0 && c + 1 < NC) {
+                __builtin_amdgcn_sched_barrier(0);
+                load(buf[(c + 1) & 1], c + 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (c + 1 < NC) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < AR; r++) asm volatile("" : "+v"(acc[r]));
+}
+
+// thread tid's window of a tile staged at s (16-byte aligned: D*AR*tid floats in)
+template <int D, int NW>
+__device__ __forceinline__ void audio_window(const float* __restrict__ s, int tid, float (&w)[NW]) {
+    static_assert((D * AR) % 4 == 0 && NW % 4 == 0, "16-byte LDS reads");
+    const float4* p = reinterpret_cast<const float4*>(s + D * AR * tid);
+#pragma unroll
+    for (int i = 0; i < NW / 4; i++) {
+        const float4 v = p[i];
+        w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+}
+
+template <int D>
+constexpr int audio_win() { return D * (ATILE - 1) + 101; }         // staged samples per tile
+template <int D>
+constexpr int audio_tw() { return (D * (AR - 1) + 101 + 3) / 4 * 4; }   // window of one thread
+
+// mono (mono.cpp:34-42): audio = short(16384 * resample(fm_demod))
+template <int D>
+__global__ __launch_bounds__(AT) void k_mono_out(const float* __restrict__ fm, size_t fm_stride,
+                                                 const float* __restrict__ h, int n, int ny,
+                                                 int16_t* __restrict__ audio, size_t audio_stride) {
+    constexpr int WIN = audio_win<D>(), TW = audio_tw<D>();
+    __shared__ __attribute__((aligned(16))) float sa[(WIN + 3) / 4 * 4 + 4];
+    const int ch = blockIdx.y, tid = threadIdx.x;
+    const int o0 = blockIdx.x * ATILE;
+    const int m0 = D * o0 - 100;
+    const float* x = fm + (size_t)ch * fm_stride;
+    const int kend = min(WIN, n - m0);                       // staged slots past the block feed only outputs >= ny
+    {
+        constexpr int NL = (WIN + AT - 1) / AT;              // every load of the tile in flight at once
+        float v[NL];
+#pragma unroll
+        for (int u = 0; u < NL; u++) {
+            const int k = tid + u * AT;
+            v[u] = k < kend ? x[m0 + k] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < NL; u++)
+            if (tid + u * AT < WIN) sa[tid + u * AT] = v[u];
+    }
+    __syncthreads();
+    const int ob = o0 + tid * AR;
+    if (ob >= ny) return;
+    float w[TW], acc[AR];
+    audio_window<D>(sa, tid, w);
+    audio_mac<D>(h, w, acc);
+    int16_t* o = audio + (size_t)ch * audio_stride + ob;
+#pragma unroll
+    for (int r = 0; r < AR; r++)
+        if (ob + r < ny) o[r] = cvt_i16_x86(16384 * acc[r]);   // mono.cpp:41
+}
+
+// ------------------------------------------------------------------------------------------
+// Stereo post stage in one pass (stereo.cpp:83-107, U == 1). The staging of an audio tile
+// computes, for every IF sample of its window, the 38 kHz carrier from the PLL phase (pll.cpp:52;
+// carrier[0] is the previous block's last), the mixer product stereo_dc = RN32(2.0 * band *
+// carrier) in f64 (stereo.cpp:83-85), and the mono delay fm[i - 50] (the 101-tap APF of :88 is
+// an exact 50-sample shift); each thread then runs both resamplers over its register windows and
+// writes L = short(16384 (m + s)), R = short(16384 (m - s)) (:100-107). The carrier and stereo_dc
+// rows never reach HBM: only stereo_dc's last HIST samples (the next block's resampler history)
+// and carrier[n] (the next block's carrier[0], and pllblock_args.lastCarrier) are stored.
+// ------------------------------------------------------------------------------------------
+struct StereoOut {
+    const float* fm;            // this parity's fm_demod, extended (fm[-HIST..n))
+    const float* band;          // band BPF output of this parity
+    const float* t;             // PLL phases of this parity
+    size_t fm_stride, plain_stride;
+    float* car;                 // carrier rows of this parity: [ch][n] written
+    const float* car_prev;      // the previous parity's: [ch][n] read
+    size_t car_stride;
+    sdr_pll_state* st;
+    float ncoScale, phaseAdjust;
+    float* sdc;                 // stereo_dc rows of this parity: the tail [n - HIST, n) written
+    const float* sdc_prev;      // the previous parity's tail: this block's history
+    size_t sdc_stride;
+    const float* h;             // the 101 audio taps
+    int n, ny;
+    int16_t* lr;
+    size_t lr_stride;
+};
+
+template <int D>
+__global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
+    constexpr int WIN = audio_win<D>(), TW = audio_tw<D>();
+    __shared__ __attribute__((aligned(16))) float sa[(WIN + 3) / 4 * 4 + 4];
+    __shared__ __attribute__((aligned(16))) float sb[(WIN + 3) / 4 * 4 + 4];
+    const int ch = blockIdx.y, tid = threadIdx.x;
+    const int o0 = blockIdx.x * ATILE;
+    const int m0 = D * o0 - 100;
+    const bool last_tile = o0 + ATILE >= a.ny;
+    // the last tile also computes up to the block end: stereo_dc's tail is the next block's history
+    const int m1 = last_tile ? a.n : min(m0 + WIN, a.n);
+    const float* fm = a.fm + (size_t)ch * a.fm_stride;
+    const float* band = a.band + (size_t)ch * a.plain_stride;
+    const float* tt = a.t + (size_t)ch * a.plain_stride;
+    const float* sprev = a.sdc_prev + (size_t)ch * a.sdc_stride;
+    float* scur = a.sdc + (size_t)ch * a.sdc_stride;
+    const float car0 = a.car_prev[(size_t)ch * a.car_stride + a.n];
+    // every load of the tile in flight at once (m1 <= m0 + WIN: the window of the last tile reaches
+    // the block end), then the carriers, mixer products and LDS writes
+    constexpr int NL = (WIN + AT - 1) / AT;
+    float vb[NL], vt[NL], vf[NL];
+#pragma unroll
+    for (int u = 0; u < NL; u++) {
+        const int i = m0 + tid + u * AT;
+        const bool in = i < m1;
+        vf[u] = in ? fm[i - 50] : 0.0f;                            // stereo.cpp:88
+        vb[u] = (in && i >= 0) ? band[i] : (in ? sprev[a.n + i] : 0.0f);   // i >= -100: history
+        vt[u] = (in && i > 0) ? tt[i - 1] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < NL; u++) {
+        const int i = m0 + tid + u * AT, k = i - m0;
+        if (i >= m1) continue;
+        float sd = vb[u];
+        if (i >= 0) {
+            const float car = (i == 0) ? car0 : nco_carrier(vt[u], a.ncoScale, a.phaseAdjust);
+            sd = (float)(2.0 * (double)vb[u] * (double)car);         // stereo.cpp:83-85
+            if (i >= a.n - HIST) scur[i] = sd;
+        }
+        sb[k] = sd;
+        sa[k] = vf[u];
+    }
+    if (last_tile && tid == 0) {                                   // carrier[n] (pll.cpp:52, :58)
+        const float cl = nco_carrier(tt[a.n - 1], a.ncoScale, a.phaseAdjust);
+        a.car[(size_t)ch * a.car_stride + a.n] = cl;
+        a.st[ch].lastCarrier = cl;
+    }
+    __syncthreads();
+    const int ob = o0 + tid * AR;
+    if (ob >= a.ny) return;
+    float w[TW], m[AR], sv[AR];
+    audio_window<D>(sa, tid, w);
+    audio_mac<D>(a.h, w, m);                                       // mono resampler (:94)
+    audio_window<D>(sb, tid, w);
+    audio_mac<D>(a.h, w, sv);                                      // stereo resampler (:97)
+    uint32_t* o = reinterpret_cast<uint32_t*>(a.lr + (size_t)ch * a.lr_stride) + ob;
+#pragma unroll
+    for (int r = 0; r < AR; r++) {
+        if (ob + r < a.ny) {
+            const uint16_t l = (uint16_t)cvt_i16_x86(16384 * (m[r] + sv[r]));   // stereo.cpp:100-102
+            const uint16_t rr = (uint16_t)cvt_i16_x86(16384 * (m[r] - sv[r]));
+            o[r] = (uint32_t)l | ((uint32_t)rr << 16);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// RDS carrier and mixer in one pass (rds.cpp:119-127): ipll[i] from the 114 kHz PLL's phase
+// (pll.cpp:52, ncoScale 0.5; ipll[0] = the previous block's last) and rds_dc[i] = (2 * delay[i]) *
+// ipll[i] in f32 with delay[i] = rds_band[i - 50] + 0 (the APF of :122 is an exact 50-sample
+// shift that turns -0 into +0) into the extended rds_dc stream, history included. ipll itself is
+// not stored: only its last sample (the next block's ipll[0], and pllblock_args.lastCarrier).
+// One thread per IF sample; thread n computes ipll[n].
+// ------------------------------------------------------------------------------------------
+struct RdsMix {
+    const float* rband;         // this parity's rds_band, extended
+    const float* t;             // PLL phases of this parity
+    size_t fm_stride, plain_stride;
+    float* car;                 // ipll rows of this parity: [ch][n] written
+    const float* car_prev;      // the previous parity's: [ch][n] read
+    size_t car_stride;
+    sdr_pll_state* st;
+    float ncoScale, phaseAdjust;
+    float* rdc;                 // this parity's rds_dc, extended (history copied by tile 0)
+    const float* rdc_prev;
+    int n;
+};
+
+__global__ __launch_bounds__(BLK) void k_rds_mix(const RdsMix a) {
+    const int ch = blockIdx.y;
+    const int i = blockIdx.x * BLK + threadIdx.x;
+    const float* tt = a.t + (size_t)ch * a.plain_stride;
+    float* y = a.rdc + (size_t)ch * a.fm_stride;
+    if (i < a.n) {
+        const float car = (i == 0) ? a.car_prev[(size_t)ch * a.car_stride + a.n]
+                                   : nco_carrier(tt[i - 1], a.ncoScale, a.phaseAdjust);
+        const float d = a.rband[(size_t)ch * a.fm_stride + i - 50] + 0.0f;    // rds.cpp:122
+        y[i] = 2 * d * car;                                                    // rds.cpp:125-127
+    } else if (i == a.n) {
+        const float cl = nco_carrier(tt[a.n - 1], a.ncoScale, a.phaseAdjust);
+        a.car[(size_t)ch * a.car_stride + a.n] = cl;
+        a.st[ch].lastCarrier = cl;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < HIST)
+        y[(int)threadIdx.x - HIST] = a.rdc_prev[(size_t)ch * a.fm_stride + a.n - HIST + threadIdx.x];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -536,7 +905,10 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
                                                  uint8_t* __restrict__ sym_out, size_t sym_stride,
                                                  int32_t* __restrict__ nbits_out, uint8_t* __restrict__ bits_out,
                                                  size_t bits_stride) {
+    // dynamic LDS: 64 cdr sums, then the channel's whole block (n floats), staged with every load in
+    // flight (the cdr reads it 39-strided and the slicer sps-strided: from LDS, not global memory)
     extern __shared__ int sums_dyn[];
+    float* xs = reinterpret_cast<float*>(sums_dyn + 64);
     __shared__ uint8_t symbols[SDR_MAX_SYMS];
     const int ch = blockIdx.x;
     const int lane = threadIdx.x;
@@ -553,11 +925,23 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
         }
         return;
     }
-    const int off = cdr_wave(xc, n, sps, sums_dyn);
+    {
+        constexpr int U = 8;                        // loads in flight per lane per round
+        for (int i0 = lane; i0 < n; i0 += 64 * U) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = (i0 + 64 * u < n) ? xc[i0 + 64 * u] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (i0 + 64 * u < n) xs[i0 + 64 * u] = v[u];
+        }
+        __syncthreads();
+    }
+    const int off = cdr_wave(xs, n, sps, sums_dyn);
     int m = 0;
     if (off < n) m = (n - off + sps - 1) / sps;     // i with off + i*sps < n
     if (m > SDR_MAX_SYMS) m = SDR_MAX_SYMS;
-    for (int i = lane; i < m; i += blockDim.x) symbols[i] = xc[off + i * sps] > 0;
+    for (int i = lane; i < m; i += blockDim.x) symbols[i] = xs[off + i * sps] > 0;
     __syncthreads();
     if (lane == 0) {
         int half_symbol = d[1], start = d[2], last_bit = d[3];
@@ -1165,10 +1549,22 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
     if (!c || !audio) return fail(SDR_E_INVALID, "null argument");
     if (c->block < 0 || c->mono_done == c->block) return fail(SDR_E_INVALID, "mono: no new block");
     const sdr_info& in = c->info;
+    const float* fm = c->fm_cur();
+    if (c->audio_u1_101 && (in.audio_decim == 5 || in.audio_decim == 9)) {   // register-blocked, modes 0 and 1
+        const dim3 g(cdiv(in.n_audio, ATILE), c->nch);
+        if (in.audio_decim == 5)
+            hipLaunchKernelGGL(k_mono_out<5>, g, dim3(AT), 0, S(stream), fm, c->fm_stride, c->audio_pp, in.block_if,
+                               in.n_audio, audio, audio_stride);
+        else
+            hipLaunchKernelGGL(k_mono_out<9>, g, dim3(AT), 0, S(stream), fm, c->fm_stride, c->audio_pp, in.block_if,
+                               in.n_audio, audio, audio_stride);
+        LAUNCH_CHECK();
+        c->mono_done = c->block;
+        return SDR_OK;
+    }
     const int tile = 512;
     dim3 grid(cdiv(in.n_audio, tile), c->nch);
     const size_t lds = resample_lds_bytes(c->audio_L, in.audio_upsample, in.audio_decim, tile, 1);
-    const float* fm = c->fm_cur();
     auto km = c->audio_u1_101 ? k_resample<1, 101> : k_resample<1, 0>;
     hipLaunchKernelGGL(km, grid, dim3(BLK), lds, S(stream), fm, fm, c->fm_stride, c->fm_stride,
                        nullptr, nullptr, (size_t)0, (size_t)0, c->audio_pp, c->audio_cnt, c->audio_L,
@@ -1182,19 +1578,38 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
 // recurrence; post: everything after it), so a caller can run the PLL of block b on its own stream
 // back to back with block b+1's while other streams do the rest. Intermediates that cross the
 // split are kept per block parity. sdr_stereo / sdr_rds_dsp run the three parts on one stream.
+extern "C++" {
+namespace {
+// launch k_fir_rb with NT tap sets (one block of every channel of length n)
+template <int NT, bool SQUARE>
+int fir_rb(const sdr_ctx* c, const float* x, size_t x_stride, int n, const FirRb& f, hipStream_t s) {
+    hipLaunchKernelGGL((k_fir_rb<NT, SQUARE>), dim3(cdiv(n, FRB_TILE), c->nch), dim3(BLK), 0, s, x, x_stride, x,
+                       x_stride, n, f);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
+// pilot BPF (stereo.cpp:74) -> pilot + its PLL reciprocals, band BPF (:80) -> band
+FirRb stereo_fir(sdr_ctx* c) {
+    FirRb f{};
+    f.h[0] = c->pilot_h;
+    f.h[1] = c->stereo_h;
+    f.y[0] = c->plain(c->pilot);
+    f.y[1] = c->plain(c->band);
+    f.y_stride[0] = f.y_stride[1] = c->plain_stride;
+    f.rx0 = c->rxbuf(c->rx_st);
+    f.rx_stride = c->plain_stride;
+    return f;
+}
+}  // namespace
+}  // extern "C++"
+
 int sdr_stereo_pre(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (c->block < 0 || c->st_pre_done == c->block) return fail(SDR_E_INVALID, "stereo_pre: no new block");
-    const sdr_info& in = c->info;
-    const int n = in.block_if, T = c->ntaps;
-    const float* fm = c->fm_cur();
+    if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "stereo_pre: %d taps", c->ntaps);
     // pilot BPF (stereo.cpp:74) + band BPF (:80) from one staged window of fm_demod
-    if (T != FRB_T) return fail(SDR_E_INVALID, "stereo_pre: %d taps", T);
-    dim3 gf(cdiv(n, FRB_TILE), c->nch);
-    hipLaunchKernelGGL((k_fir_rb<2, false>), gf, dim3(BLK), 0, S(stream), fm, c->fm_stride, fm, c->fm_stride,
-                       c->pilot_h, c->stereo_h, n, c->plain(c->pilot), c->plain(c->band), c->plain_stride,
-                       c->rxbuf(c->rx_st), c->plain_stride);
-    LAUNCH_CHECK();
+    const int r = fir_rb<2, false>(c, c->fm_cur(), c->fm_stride, c->info.block_if, stereo_fir(c), S(stream));
+    if (r) return r;
     c->st_pre_done = c->block;
     return SDR_OK;
 }
@@ -1219,6 +1634,39 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
     hipStream_t s = S(stream);
     const int n = in.block_if;
     const float* fm = c->fm_cur();
+    if (!(c->flags & SDR_FLAG_KEEP_INTERMEDIATES) && c->audio_u1_101 &&
+        (in.audio_decim == 5 || in.audio_decim == 9)) {
+        // NCO, mixer, mono delay, both resamplers and L/R in one pass (k_stereo_out)
+        const int p = c->parity;
+        StereoOut a{};
+        a.fm = fm;
+        a.band = c->plain(c->band);
+        a.t = c->plain(c->t_st);
+        a.fm_stride = c->fm_stride;
+        a.plain_stride = c->plain_stride;
+        a.car = c->pllbuf(c->carrier);
+        a.car_prev = c->carrier + (p ^ 1) * c->pll_par;
+        a.car_stride = c->pll_stride;
+        a.st = c->st_pll;
+        a.ncoScale = 2.0f;                          // stereo.cpp:77: fmpll(..., 2.0, 0, 0.01)
+        a.phaseAdjust = 0.0f;
+        a.sdc = c->sdc + p * c->fm_par;
+        a.sdc_prev = c->sdc + (p ^ 1) * c->fm_par;
+        a.sdc_stride = c->fm_stride;
+        a.h = c->audio_pp;
+        a.n = n;
+        a.ny = in.n_audio;
+        a.lr = lr;
+        a.lr_stride = lr_stride;
+        const dim3 g(cdiv(in.n_audio, ATILE), c->nch);
+        if (in.audio_decim == 5)
+            hipLaunchKernelGGL(k_stereo_out<5>, g, dim3(AT), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_stereo_out<9>, g, dim3(AT), 0, s, a);
+        LAUNCH_CHECK();
+        c->stereo_done = c->block;
+        return SDR_OK;
+    }
     {
         // NCO output of this block's PLL phases (pll.cpp:52), carrier[0] = last of the previous block
         PllJobs jobs{};
@@ -1255,29 +1703,63 @@ int sdr_stereo(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
     return r;
 }
 
+extern "C++" {
+namespace {
+// squaring (rds.cpp:111-113) + 114 kHz BPF (:116) of the extended rds_band stream -> gen_pilot + its
+// PLL reciprocals
+int rds_sq_fir(sdr_ctx* c, hipStream_t s) {
+    FirRb f{};
+    f.h[0] = c->rds_sq_h;
+    f.y[0] = c->plain(c->gpilot);
+    f.y_stride[0] = c->plain_stride;
+    f.rx0 = c->rxbuf(c->rx_rds);
+    f.rx_stride = c->plain_stride;
+    return fir_rb<1, true>(c, c->rband + c->parity * c->fm_par, c->fm_stride, c->info.block_if, f, s);
+}
+}  // namespace
+}  // extern "C++"
+
 int sdr_rds_pre(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (c->block < 0 || c->rds_pre_done == c->block) return fail(SDR_E_INVALID, "rds_pre: no new block");
-    const sdr_info& in = c->info;
+    if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "rds_pre: %d taps", c->ntaps);
     hipStream_t s = S(stream);
-    const int n = in.block_if, T = c->ntaps, p = c->parity;
-    const float* fm = c->fm_cur();
+    const int n = c->info.block_if, p = c->parity;
     float* rband = c->rband + p * c->fm_par;
-    if (T != FRB_T) return fail(SDR_E_INVALID, "rds_pre: %d taps", T);
-    dim3 gf(cdiv(n, FRB_TILE), c->nch);
     // RDS band BPF (rds.cpp:105) into the extended rds_band stream
     hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rband, c->rband + (p ^ 1) * c->fm_par,
                        c->fm_stride, n);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL((k_fir_rb<1, false>), gf, dim3(BLK), 0, s, fm, c->fm_stride, fm, c->fm_stride, c->rds_h,
-                       nullptr, n, rband, nullptr, c->fm_stride, nullptr, 0);
-    LAUNCH_CHECK();
-    // squaring (:111-113) + 114 kHz BPF (:116)
-    hipLaunchKernelGGL((k_fir_rb<1, true>), gf, dim3(BLK), 0, s, rband, c->fm_stride, rband, c->fm_stride,
-                       c->rds_sq_h, nullptr, n, c->plain(c->gpilot), nullptr, c->plain_stride,
-                       c->rxbuf(c->rx_rds), c->plain_stride);
-    LAUNCH_CHECK();
+    FirRb f{};
+    f.h[0] = c->rds_h;
+    f.y[0] = rband;
+    f.y_stride[0] = c->fm_stride;
+    int r = fir_rb<1, false>(c, c->fm_cur(), c->fm_stride, n, f, s);
+    if (!r) r = rds_sq_fir(c, s);
+    if (r) return r;
     c->rds_pre_done = c->block;
+    return SDR_OK;
+}
+
+int sdr_pre(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->block < 0 || c->st_pre_done == c->block || c->rds_pre_done == c->block)
+        return fail(SDR_E_INVALID, "pre: no new block");
+    if (!c->rds_on) return sdr_stereo_pre(c, stream);
+    if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "pre: %d taps", c->ntaps);
+    hipStream_t s = S(stream);
+    const int n = c->info.block_if, p = c->parity;
+    // pilot, band and RDS band BPFs (stereo.cpp:74,80, rds.cpp:105) from one staged fm_demod window;
+    // the third output goes into the extended rds_band stream, history included
+    FirRb f = stereo_fir(c);
+    f.h[2] = c->rds_h;
+    f.y[2] = c->rband + p * c->fm_par;
+    f.y_stride[2] = c->fm_stride;
+    f.hist2_src = c->rband + (p ^ 1) * c->fm_par;
+    int r = fir_rb<3, false>(c, c->fm_cur(), c->fm_stride, n, f, s);
+    if (!r) r = rds_sq_fir(c, s);
+    if (r) return r;
+    c->st_pre_done = c->rds_pre_done = c->block;
     return SDR_OK;
 }
 
@@ -1463,16 +1945,36 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
     float* rband = c->rband + p * c->fm_par;
     float* rdc = c->rdc + p * c->fm_par;
     float* rfilt = c->rfilt + p * c->rf_par;
-    {
-        PllJobs jobs{};
-        jobs.j[0] = rds_job(c);                       // NCO output of this block's PLL (rds.cpp:119)
-        const int r = launch_nco(jobs, 1, n, c->nch, s);
-        if (r) return r;
+    if (!(c->flags & SDR_FLAG_KEEP_INTERMEDIATES)) {
+        // NCO (rds.cpp:119, pll.cpp:52) + delay (:122) + mixer (:125-127) in one pass (k_rds_mix)
+        RdsMix a{};
+        a.rband = rband;
+        a.t = c->plain(c->t_rds);
+        a.fm_stride = c->fm_stride;
+        a.plain_stride = c->plain_stride;
+        a.car = c->pllbuf(c->ipll);
+        a.car_prev = c->ipll + (p ^ 1) * c->pll_par;
+        a.car_stride = c->pll_stride;
+        a.st = c->rds_pll;
+        a.ncoScale = 0.5f;                          // rds.cpp:119: fmpll(..., 0.5, 0, 0.001)
+        a.phaseAdjust = 0.0f;
+        a.rdc = rdc;
+        a.rdc_prev = c->rdc + (p ^ 1) * c->fm_par;
+        a.n = n;
+        hipLaunchKernelGGL(k_rds_mix, dim3(cdiv(n + 1, BLK), c->nch), dim3(BLK), 0, s, a);
+        LAUNCH_CHECK();
+    } else {
+        {
+            PllJobs jobs{};
+            jobs.j[0] = rds_job(c);                   // NCO output of this block's PLL (rds.cpp:119)
+            const int r = launch_nco(jobs, 1, n, c->nch, s);
+            if (r) return r;
+        }
+        // delay (rds.cpp:122) + mixer (:125-127) into the extended rds_dc stream
+        hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride,
+                           c->pllbuf(c->ipll), c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
+        LAUNCH_CHECK();
     }
-    // delay (rds.cpp:122) + mixer (:125-127) into the extended rds_dc stream
-    hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride,
-                       c->pllbuf(c->ipll), c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
-    LAUNCH_CHECK();
     // 247/640 resampler (:130) into the extended rds_filt stream
     hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rfilt, c->rfilt + (p ^ 1) * c->rf_par,
                        c->rf_stride, in.n_rds);
@@ -1486,13 +1988,17 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
                        rfilt, c->rf_stride);
     LAUNCH_CHECK();
     // RRC (:133)
-    dim3 gc(cdiv(in.n_rds, FRB_TILE), c->nch);
     float* dst = rds_clean ? rds_clean : c->rds_clean;
     const size_t dst_stride = rds_clean ? rds_stride : c->clean_stride;
     if (T != FRB_T) return fail(SDR_E_INVALID, "rds_post: %d taps", T);
-    hipLaunchKernelGGL((k_fir_rb<1, false>), gc, dim3(BLK), 0, s, rfilt, c->rf_stride, rfilt, c->rf_stride,
-                       c->rrc_h, nullptr, in.n_rds, dst, nullptr, dst_stride, nullptr, 0);
-    LAUNCH_CHECK();
+    {
+        FirRb f{};
+        f.h[0] = c->rrc_h;
+        f.y[0] = dst;
+        f.y_stride[0] = dst_stride;
+        const int r = fir_rb<1, false>(c, rfilt, c->rf_stride, in.n_rds, f, s);
+        if (r) return r;
+    }
     if (rds_clean) {
         HIP_TRY(hipMemcpy2DAsync(c->rds_clean, c->clean_stride * sizeof(float), rds_clean, rds_stride * sizeof(float),
                                  in.n_rds * sizeof(float), c->nch, hipMemcpyDeviceToDevice, s));
@@ -1516,7 +2022,8 @@ int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, s
     if (c->rds_dsp_done != c->block || c->rds_bits_done == c->block)
         return fail(SDR_E_INVALID, "rds_bits: run sdr_rds_dsp on a new block first");
     const sdr_info& in = c->info;
-    hipLaunchKernelGGL(k_rds_bits, dim3(c->nch), dim3(64), 64 * sizeof(int), S(stream), c->rds_clean,
+    hipLaunchKernelGGL(k_rds_bits, dim3(c->nch), dim3(64), 64 * sizeof(int) + (size_t)in.n_rds * sizeof(float),
+                       S(stream), c->rds_clean,
                        c->clean_stride, in.n_rds, in.symbol_Fs, c->rds_on, c->dec, offset, nsym, symbols,
                        sym_stride, nbits, bits, bits_stride);
     LAUNCH_CHECK();

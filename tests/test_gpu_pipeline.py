@@ -189,8 +189,8 @@ def test_fast_pll_matches_libm_pll(pkg, synth, torch_cuda):
     nch, nb = 48, 40
     iqs = [channel_input(synth, 200 + c, nb) for c in range(nch)]
     d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
-    pa = pkg.Pipeline(nch)
-    pb = pkg.Pipeline(nch, flags=pkg.FLAG_PLL_LIBM)
+    pa = pkg.Pipeline(nch, flags=pkg.FLAG_KEEP_INTERMEDIATES)
+    pb = pkg.Pipeline(nch, flags=pkg.FLAG_PLL_LIBM | pkg.FLAG_KEEP_INTERMEDIATES)
     for b in range(nb):
         for p in (pa, pb):
             p.frontend(d[b])
@@ -200,6 +200,35 @@ def test_fast_pll_matches_libm_pll(pkg, synth, torch_cuda):
             xa, xb = pa.buffer(name).cpu().numpy(), pb.buffer(name).cpu().numpy()
             assert np.array_equal(xa.view(np.uint32), xb.view(np.uint32)), f"{name} block {b}"
         assert torch.equal(pa.nbits, pb.nbits) and torch.equal(pa.bits, pb.bits)
+    pa.close()
+    pb.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_fused_post_stages_match_unfused(pkg, synth, torch_cuda, mode):
+    """The default post stages (NCO + mixer + mono delay + both audio resamplers in one kernel;
+    NCO + delay + mixer in one kernel for RDS; register-blocked mono resampler) against the
+    unfused kernels that store every intermediate row (SDR_FLAG_KEEP_INTERMEDIATES): identical
+    mono, stereo, rds_clean and RDS bits, block by block (stereo.cpp:83-107, rds.cpp:119-127,
+    mono.cpp:34-42). Mode 0 resamples by 5, mode 1 by 9, mode 2 by 147/800 (unfused stereo path)."""
+    torch = torch_cuda
+    nch, nb = 24, 12
+    pa = pkg.Pipeline(nch, mode=mode)
+    pb = pkg.Pipeline(nch, mode=mode, flags=pkg.FLAG_KEEP_INTERMEDIATES)
+    info = pa.info
+    srcs = [synth.FMMultiplexSource(700 + c) for c in range(nch)]
+    for b in range(nb):
+        d = torch.from_numpy(np.stack([s_.next_block(info.block_iq) for s_ in srcs])).cuda()
+        outs = []
+        for p in (pa, pb):
+            p.frontend(d)
+            outs.append((p.mono().cpu().numpy(), p.stereo().cpu().numpy(), p.rds().cpu().numpy(),
+                         p.nbits.cpu().numpy().copy(), p.bits.cpu().numpy().copy()))
+        for k, name in enumerate(("mono", "stereo", "rds_clean", "nbits", "bits")):
+            x, y = outs[0][k], outs[1][k]
+            if x.dtype == np.float32:
+                x, y = x.view(np.uint32), y.view(np.uint32)
+            assert np.array_equal(x, y), f"mode {mode} block {b}: {name}"
     pa.close()
     pb.close()
 

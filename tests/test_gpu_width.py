@@ -115,8 +115,7 @@ def _run_schedule(torch, pkg, bench, iq, dev, schedule: str) -> dict:
         pipe.frontend(iq[b], stream=s_fe)
         pipe.fm_demod(cap["fm"][b], stream=s_fe)
         pipe.mono(cap["mono"][b], stream=s_fe)
-        pipe.stereo_pre(stream=s_fe)
-        pipe.rds_pre(stream=s_fe)
+        pipe.pre(stream=s_fe)                              # stereo_pre + rds_pre, one staged window
         if persistent:
             pipe.plls_signal(stream=s_fe)
             pipe.plls_wait(stream=s_post)

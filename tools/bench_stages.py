@@ -2,7 +2,7 @@
 """Isolated timing of every stage of the exact pipeline on ONE stream (each kernel alone on the
 chip), with each stage's VALU or HBM floor beside it.
 
-One iteration = one block of every channel: frontend, mono, stereo_pre, rds_pre, plls (per-block
+One iteration = one block of every channel: frontend, mono, pre (stereo_pre + rds_pre), plls (per-block
 dispatch), stereo_post, rds_post + rds_bits. HIP events bracket each stage over `iters` blocks of
 distinct resident input; under `rocprofv3 --kernel-trace --stats` the same run gives per-kernel
 isolated durations, and under `--pmc` the per-kernel counters (tools/gpu/stage_pmc.sh).
@@ -32,8 +32,7 @@ def floors(info, nch: int) -> dict:
     ops = {
         "frontend": nch * info.block_if * 2 * mac,                        # I and Q, decimated outputs
         "mono": nch * info.n_audio * mac,
-        "stereo_pre": nch * n * 2 * mac,                                   # pilot + band BPFs
-        "rds_pre": nch * n * 2 * mac,                                      # RDS BPF + squared BPF
+        "pre": nch * n * 4 * mac,                                          # pilot, band, RDS, squared-RDS BPFs
         "stereo_post": nch * info.n_audio * 2 * mac,                       # two resamplers (+ NCO, mixer)
         "rds_post": nch * info.n_rds * 2 * mac,                            # 247/640 resampler + RRC (+ NCO, mixer)
     }
@@ -57,14 +56,13 @@ def main() -> None:
     mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
     lr = torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev)
     clean = torch.empty(nch, info.n_rds, dtype=torch.float32, device=dev)
-    stages = ("frontend", "mono", "stereo_pre", "rds_pre", "plls", "stereo_post", "rds_post")
+    stages = ("frontend", "mono", "pre", "plls", "stereo_post", "rds_post")
     ev = {k: [] for k in stages}
 
     def one(b: int, timed: bool) -> None:
         calls = (("frontend", lambda: pipe.frontend(iq[b % args.blocks], stream=s)),
                  ("mono", lambda: pipe.mono(mono, stream=s)),
-                 ("stereo_pre", lambda: pipe.stereo_pre(stream=s)),
-                 ("rds_pre", lambda: pipe.rds_pre(stream=s)),
+                 ("pre", lambda: pipe.pre(stream=s)),
                  ("plls", lambda: pipe.plls(stream=s)),
                  ("stereo_post", lambda: pipe.stereo_post(lr, stream=s)),
                  ("rds_post", lambda: pipe.rds_post(clean, bits=True, stream=s)))
