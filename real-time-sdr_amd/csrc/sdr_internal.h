@@ -72,6 +72,8 @@ struct PllJob {
     // pll_math.h pll_rx of every input sample (written by the producer of `in`)
     const double* rx;
     size_t rx_stride;
+    // -in, same layout (written by the producer): with it the PLL runs on lane pairs (sdr_pll.hip)
+    const float* in_neg;
 };
 struct PllJobs {
     PllJob j[2];
@@ -146,6 +148,7 @@ struct sdr_ctx {
     size_t fm_stride = 0, rf_stride = 0;               // per-channel strides (if, rds lengths)
     size_t fm_par = 0, rf_par = 0;                      // parity offsets in elements
     // plain per-block buffers
+    float *pilot_neg = nullptr, *gpilot_neg = nullptr;  // -pilot, -gen_pilot (the lane-pair PLL's input)
     float *pilot = nullptr, *band = nullptr, *gpilot = nullptr, *carrier = nullptr, *ipll = nullptr,
           *rds_clean = nullptr, *t_st = nullptr, *t_rds = nullptr;
     int* rds_ptq = nullptr;                             // RDS resampler (q << 8 | phase) per output

@@ -132,12 +132,14 @@ constexpr int FRB_TILE = BLK * FRB_R;      // outputs per workgroup
 constexpr int FRB_W = FRB_TILE + FRB_T - 1 + 3;   // staged samples (+3: whole 16-byte reads)
 
 // Up to three tap sets over one input window. Output t goes to y[t] (stride y_stride[t]); y[0] may
-// also get its PLL reciprocals (rx0), and y[2] the history of an extended stream (hist2_src: the
-// other parity's row, copied in front by the first tile of each channel).
+// also get its PLL reciprocals (rx0) and its negation (y0neg, same stride: the lane-pair PLL's
+// second input, sdr_pll.hip pll_run_split), and y[2] the history of an extended stream (hist2_src:
+// the other parity's row, copied in front by the first tile of each channel).
 struct FirRb {
     const float* h[3];
     float* y[3];
     size_t y_stride[3];
+    float* y0neg;
     double* rx0;
     size_t rx_stride;
     const float* hist2_src;
@@ -247,6 +249,18 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
 #pragma unroll
             for (int j = 0; j < R; j++)
                 if (nb + j < ny) o[j] = a[t][j];
+        }
+    }
+    if (f.y0neg) {                                                // y[0] feeds a PLL: -y[0]
+        float* o = f.y0neg + (size_t)ch * f.y_stride[0] + nb;
+        if (nb + R <= ny) {
+#pragma unroll
+            for (int j = 0; j < R; j += 4)
+                reinterpret_cast<float4*>(o + j)[0] = make_float4(-a[0][j], -a[0][j + 1], -a[0][j + 2], -a[0][j + 3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < R; j++)
+                if (nb + j < ny) o[j] = -a[0][j];
         }
     }
     if (f.rx0) {                                                  // y[0] feeds a PLL: its reciprocal
@@ -1181,13 +1195,15 @@ PllJob stereo_job(sdr_ctx* c) {   // stereo.cpp:77: fmpll(pilot, 19e3, rf_Fs/rf_
     const sdr_info& in = c->info;
     return PllJob{c->plain(c->pilot), c->plain_stride, c->plain(c->t_st), c->plain_stride, c->pllbuf(c->carrier),
                   c->pll_stride, c->st_pll, 19e3f, (float)(in.rf_Fs / in.rf_decim), 0.01f, 2.0f, 0.0f,
-                  c->carrier + (c->parity ^ 1) * c->pll_par, c->rxbuf(c->rx_st), c->plain_stride};
+                  c->carrier + (c->parity ^ 1) * c->pll_par, c->rxbuf(c->rx_st), c->plain_stride,
+                  c->plain(c->pilot_neg)};
 }
 PllJob rds_job(sdr_ctx* c) {      // rds.cpp:119: fmpll(gen_pilot, 114e3, if_Fs, ..., 0.5, 0, 0.001)
     const sdr_info& in = c->info;
     return PllJob{c->plain(c->gpilot), c->plain_stride, c->plain(c->t_rds), c->plain_stride, c->pllbuf(c->ipll),
                   c->pll_stride, c->rds_pll, 114e3f, (float)in.if_Fs, 0.001f, 0.5f, 0.0f,
-                  c->ipll + (c->parity ^ 1) * c->pll_par, c->rxbuf(c->rx_rds), c->plain_stride};
+                  c->ipll + (c->parity ^ 1) * c->pll_par, c->rxbuf(c->rx_rds), c->plain_stride,
+                  c->plain(c->gpilot_neg)};
 }
 
 }  // namespace
@@ -1445,6 +1461,8 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     TRY(dalloc(c, &c->pilot, 2 * c->plain_par));
     TRY(dalloc(c, &c->band, 2 * c->plain_par));
     TRY(dalloc(c, &c->gpilot, 2 * c->plain_par));
+    TRY(dalloc(c, &c->pilot_neg, 2 * c->plain_par));
+    TRY(dalloc(c, &c->gpilot_neg, 2 * c->plain_par));
     TRY(dalloc(c, &c->t_st, 2 * c->plain_par));
     TRY(dalloc(c, &c->t_rds, 2 * c->plain_par));
     {
@@ -1598,6 +1616,7 @@ FirRb stereo_fir(sdr_ctx* c) {
     f.y_stride[0] = f.y_stride[1] = c->plain_stride;
     f.rx0 = c->rxbuf(c->rx_st);
     f.rx_stride = c->plain_stride;
+    f.y0neg = c->plain(c->pilot_neg);
     return f;
 }
 }  // namespace
@@ -1714,6 +1733,7 @@ int rds_sq_fir(sdr_ctx* c, hipStream_t s) {
     f.y_stride[0] = c->plain_stride;
     f.rx0 = c->rxbuf(c->rx_rds);
     f.rx_stride = c->plain_stride;
+    f.y0neg = c->plain(c->gpilot_neg);
     return fir_rb<1, true>(c, c->rband + c->parity * c->fm_par, c->fm_stride, c->info.block_if, f, s);
 }
 }  // namespace

@@ -81,6 +81,7 @@ __device__ __forceinline__ PllRegs pll_load(const sdr_pll_state& st, double w) {
 //     |phaseEst| < 2^28 plus 16 steps of drift; without it the chunk's largest |t| is tracked.
 struct PllProof {
     double emax = 0.0;
+    float emaxf = 0.0f;     // lane-pair steps: max |RN32(ed)| (PLL_EMAX_F)
     uint32_t split = 0u;
     uint32_t tie = ~0u;
     float tmax = 0.0f;
@@ -99,6 +100,9 @@ struct PllProof {
 #endif
 // |e| bound of the fast phase detector (the wrap to [-pi, pi] is the reference's below it)
 constexpr double PLL_EMAX = SDR_PLL_EDHI ? pllm::PI - 0x1p-30 - 0x1p-42 : pllm::PI - 0x1p-30;
+// the largest f32 below PLL_EMAX: RN32 is monotone, so |RN32(ed)| < PLL_EMAX_F implies |ed| < PLL_EMAX_F
+constexpr float PLL_EMAX_F = __builtin_bit_cast(float, 0x40490FDAu);
+static_assert((double)PLL_EMAX_F < PLL_EMAX, "PLL_EMAX_F");
 constexpr double PLL_TAB_WT_MAX = 0x1.6p29;   // |w * trigOffset| bound of the table path (above)
 
 #ifndef SDR_PLL_COUNT
@@ -430,14 +434,281 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
     st[ch].trigOffset = r.toff;
 }
 
+// ------------------------------------------------------------------------------------------
+// The PLL step on a LANE PAIR (SPLIT). One lane's step issues ~50 instructions, one per quad-cycle
+// for a lone wave, and half of them are the two kernels of cos r and sin r and their roundings and
+// tie keys. Here lanes 2k and 2k+1 both run channel k: the even lane (A) evaluates cos r, the odd
+// lane (B) sin r -- the same instruction stream, f = u + z u P(z) with per-lane coefficients
+// (A: u = 1, P = the cos kernel's; B: u = r, P = fdlibm's sin kernel) -- and the phase detector
+// takes the partner's value across the pair with DPP:
+//   g = RN32(xs * fb_partner)   A: xs = -x, RN32(-x fQ0) = eQ0    B: xs = x, RN32(x fI0) = eI0
+//   q = g * f_own               A: eQ0 c                          B: eI0 s
+//   Y = q + q_partner           eI0 s + eQ0 c on both lanes (the same two f64 products, one sum)
+// (pll.cpp:36-39 in the reduced frame, pll_math.h phase_detect2; xs = -x comes from the producer:
+// the sign of eQ0 cannot otherwise enter one lane only). e, the loop filter, t, the reduction and
+// the proof accumulators are identical on both lanes; the e bracket is proven half on each lane
+// (A: RN32(ed - eps) = e, B: RN32(ed + eps) = e) and each lane proves its own f32 rounding tie, so
+// a chunk is accepted only when both lanes of the pair accept it. A redo runs the full checked
+// step (pll_step<true>) on both lanes of the pair with the exchanged values.
+// ------------------------------------------------------------------------------------------
+struct SplitRegs {
+    double f;        // A: cos r, B: sin r (f64)
+    float fb;        // RN32(f): A: fI0, B: fQ0 (reduced frame)
+    f32x2 ip;        // {integrator, phaseEst}
+    double toff;
+    double mr;       // -r
+    uint32_t nq1, b; // 1 - q, [r < 0]
+};
+
+struct SplitLane {
+    double c0, c1, c2, c3, c4, c5;   // P(z) = c0 + c1 z + ... + c5 z^5
+    double k1, k0;                   // u = k1 r + k0
+    double eps;                      // the end of the e bracket this lane proves
+    bool a;                          // even lane: cos
+};
+
+__device__ __forceinline__ SplitLane split_lane() {
+    SplitLane L;
+    L.a = (threadIdx.x & 1) == 0;
+    if (L.a) {   // cos r = 1 + z (-1/2 + C1 z + ... + C5 z^5) (pll_math.h, refitted)
+        L.c0 = -0.5; L.c1 = pllm::C1; L.c2 = pllm::C2; L.c3 = pllm::C3; L.c4 = pllm::C4; L.c5 = pllm::C5;
+        L.k1 = 0.0; L.k0 = 1.0; L.eps = -pllm::EPS_ABS_E2;
+    } else {     // sin r = r + r z (S1 + S2 z + ... + S6 z^5) (fdlibm k_sin)
+        L.c0 = pllm::S1; L.c1 = pllm::S2; L.c2 = pllm::S3; L.c3 = pllm::S4; L.c4 = pllm::S5; L.c5 = pllm::S6;
+        L.k1 = 1.0; L.k0 = 0.0; L.eps = pllm::EPS_ABS_E2;
+    }
+    return L;
+}
+
+// value of the other lane of the pair (DPP quad_perm [1,0,3,2])
+__device__ __forceinline__ float pair_swap(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double pair_swap(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0xB1, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0xB1, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ PllRegs split_to_full(const SplitRegs& s, bool a) {
+    PllRegs r;
+    const double fo = pair_swap(s.f);
+    const float fbo = pair_swap(s.fb);
+    r.c = a ? s.f : fo;
+    r.s = a ? fo : s.f;
+    r.fbI = a ? s.fb : fbo;
+    r.fbQ = a ? fbo : s.fb;
+    r.ip = s.ip;
+    r.toff = s.toff;
+    r.mr = s.mr;
+    r.nq1 = s.nq1;
+    r.b = s.b;
+    return r;
+}
+
+__device__ __forceinline__ SplitRegs full_to_split(const PllRegs& r, bool a) {
+    SplitRegs s;
+    s.f = a ? r.c : r.s;
+    s.fb = a ? r.fbI : r.fbQ;
+    s.ip = r.ip;
+    s.toff = r.toff;
+    s.mr = r.mr;
+    s.nq1 = r.nq1;
+    s.b = r.b;
+    return s;
+}
+
+template <bool TAB>
+__device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx, float Kp, float Ki, double w,
+                                               double wt, float& t_out, PllProof& pf, const SplitLane& L) {
+    // pll.cpp:36-39 across the pair (see above)
+    const float g = xs * pair_swap(r.fb);
+    const double q = (double)g * r.f;
+    const double Y = q + pair_swap(q);
+    const double base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
+    const double ed = pllm::fma_(Y, rx, base);
+    const float e = (float)ed;                                     // = RN32(atan2) when proven
+    pf.emaxf = fmaxf(pf.emaxf, __builtin_fabsf(e));               // f32: two steps per v_max3_f32
+    pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, (float)(ed + L.eps)), __builtin_bit_cast(uint32_t, e));
+    {   // pll.cpp:41-42
+        const float ki_e = Ki * e;
+        const float integ = r.ip.x + ki_e;
+        r.ip.y = (r.ip.y + Kp * e) + integ;
+        r.ip.x = integ;
+    }
+    float t;
+    if (TAB) {
+        t = (float)(wt + (double)r.ip.y);                         // pll.cpp:47
+    } else {
+        r.toff += 1.0;                                             // pll.cpp:46
+        t = (float)(w * r.toff + (double)r.ip.y);
+    }
+    // reduction (pll_math.h sincos_rn) and this lane's kernel
+    const double x = (double)t;
+    const double kdp = pllm::fma_(x, -pllm::TWO_OVER_PI, pllm::MAGIC1);
+    const double kdn = kdp - pllm::MAGIC1;
+    const double rr = pllm::fma_(kdn, pllm::PIO2_LO, pllm::fma_(kdn, pllm::PIO2_HI, x));
+    r.nq1 = (uint32_t)__builtin_bit_cast(uint64_t, kdp);
+    r.b = (uint32_t)(__builtin_bit_cast(uint64_t, rr) >> 63);
+    r.mr = -rr;
+    const double z = rr * rr, z2 = z * z;
+    const double P = pllm::fma_(z2, pllm::fma_(z2, pllm::fma_(z, L.c5, L.c4), pllm::fma_(z, L.c3, L.c2)),
+                                pllm::fma_(z, L.c1, L.c0));
+    const double u = pllm::fma_(rr, L.k1, L.k0);
+    r.f = pllm::fma_(z * u, P, u);
+    r.fb = (float)r.f;                                             // pll.cpp:49-50, reduced frame
+    pf.tie = min(pf.tie, pllm::tie_key64(r.f));                   // this lane's rounding (pll_math.h)
+    if (!TAB) pf.tmax = fmaxf(pf.tmax, __builtin_fabsf(t));
+    t_out = t;
+}
+
+// pll_run on lane pairs: ch = channel of the pair, xneg = -x row of the producer (lane A's input)
+template <bool VEC, bool TAB>
+__device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, const double* __restrict__ wtab) {
+    const SplitLane L = split_lane();
+    const size_t in_stride = jb.in_stride, t_stride = jb.t_stride, out_stride = jb.out_stride;
+    sdr_pll_state* __restrict__ st = jb.st;
+    const float freq = jb.freq, Fs = jb.Fs, normBandwidth = jb.bw;
+    const float Cp = 2.666;
+    const float Ci = 3.555;
+    const float Kp = normBandwidth * Cp;
+    const float Ki = normBandwidth * normBandwidth * Ci;
+    const double w = 2 * 3.14159265358979323846 * (freq / Fs);
+    const sdr_pll_state s0 = st[ch];
+    const float* xpos = jb.in + (size_t)ch * in_stride;
+    const float* xs = (L.a ? jb.in_neg : jb.in) + (size_t)ch * in_stride;   // lane A: -x
+    const double* rxp = jb.rx + (size_t)ch * jb.rx_stride;
+    float* tb = jb.tbuf + (size_t)ch * t_stride;
+    if (!jb.prev_out && L.a) jb.out[(size_t)ch * out_stride] = s0.lastCarrier;   // pll.cpp:18
+    SplitRegs r = full_to_split(pll_load(s0, w), L.a);
+    constexpr int C = PLL_CHUNK, NB = PLL_NBUF;
+    const int nchunks = n / C;
+    const int nmain = nchunks - nchunks % NB;
+    float xb[NB][C];
+    double rb[NB][C];
+    auto load_chunk = [&](float* dx, double* dr, int i0) {
+        if (VEC) {
+#pragma unroll
+            for (int k = 0; k < C / 4; k++) {
+                const float4 v = reinterpret_cast<const float4*>(xs + i0)[k];
+                dx[4 * k] = v.x; dx[4 * k + 1] = v.y; dx[4 * k + 2] = v.z; dx[4 * k + 3] = v.w;
+            }
+#pragma unroll
+            for (int k = 0; k < C / 2; k++) {
+                const double2 v = reinterpret_cast<const double2*>(rxp + i0)[k];
+                dr[2 * k] = v.x; dr[2 * k + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < C; k++) {
+                dx[k] = xs[i0 + k];
+                dr[k] = rxp[i0 + k];
+            }
+        }
+    };
+    if (nmain > 0) {
+#pragma unroll
+        for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
+    }
+    for (int c0 = 0; c0 < nmain; c0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; u++) {
+            const int i0 = (c0 + u) * C;
+            double wv[C];
+            if (TAB) {
+#pragma unroll
+                for (int k = 0; k < C / 2; k++) {
+                    const double2 v = reinterpret_cast<const double2*>(wtab + i0)[k];
+                    wv[2 * k] = v.x; wv[2 * k + 1] = v.y;
+                }
+            }
+            const SplitRegs snap = r;
+            PllProof pf;
+            float tv[C];
+#pragma unroll
+            for (int j = 0; j < C; j++)
+                pll_step_split<TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf, L);
+            // this lane's proof: its half of the e bracket, the e range, its own rounding ties, and
+            // the state range (a NaN from an invalid input fails it)
+            const bool ok = (pf.emaxf < PLL_EMAX_F) & (pf.split == 0u) & (pf.tie > pllm::TIE_MIN) &
+                            (__builtin_fabs(r.ip.y) < 0x1p28f) & (__builtin_fabs(r.ip.x) < 0x1p20f) &
+                            (TAB || (pf.tmax < 0x1p30f));
+#if SDR_PLL_COUNT
+            pll_count_chunk(ok);
+#endif
+            // the partner's verdict, read with every lane of the pair active (under `ok && ...` the
+            // exchange would sit in a branch, and a lane reading a disabled partner keeps its own value)
+            const int ok_partner = __builtin_amdgcn_mov_dpp((int)ok, 0xB1, 0xF, 0xF, false);
+            const bool pair_ok = ok & (ok_partner != 0);
+            if (!pair_ok) {
+                PllRegs full = split_to_full(snap, L.a);
+#pragma unroll
+                for (int j = 0; j < C; j++)
+                    pll_step<true, TAB>(full, L.a ? -xb[u][j] : xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0,
+                                        tv[j], pf);
+                r = full_to_split(full, L.a);
+            }
+            if (VEC) {
+#pragma unroll
+                for (int k = 0; k < C / 4; k++)
+                    reinterpret_cast<float4*>(tb + i0)[k] = make_float4(tv[4 * k], tv[4 * k + 1], tv[4 * k + 2], tv[4 * k + 3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
+            }
+            load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
+        }
+    }
+    PllRegs full = split_to_full(r, L.a);
+    {
+        // the rest (< NB chunks + n % C steps): full checked steps on both lanes of the pair
+        PllProof pf;
+        const int i_rest = nmain * C;
+        float xr[C];
+        double rr[C], wr[C];
+        auto load_rest = [&](int i0) {
+#pragma unroll
+            for (int k = 0; k < C; k++) {
+                const int i = min(i0 + k, n - 1);
+                xr[k] = xpos[i];
+                rr[k] = rxp[i];
+                wr[k] = TAB ? wtab[i] : 0.0;
+            }
+        };
+        if (i_rest < n) load_rest(i_rest);
+        for (int i0 = i_rest; i0 < n; i0 += C) {
+            float xc[C];
+            double rc[C], wc[C];
+#pragma unroll
+            for (int k = 0; k < C; k++) { xc[k] = xr[k]; rc[k] = rr[k]; wc[k] = wr[k]; }
+            if (i0 + C < n) load_rest(i0 + C);
+#pragma unroll
+            for (int k = 0; k < C; k++)
+                if (i0 + k < n) pll_step<true, TAB>(full, xc[k], rc[k], Kp, Ki, w, wc[k], tb[i0 + k], pf);
+        }
+    }
+    if (TAB) full.toff = s0.trigOffset + (double)n;            // pll.cpp:46, n times (exact)
+    if (L.a) {   // every field but lastCarrier (the NCO's); the feedback back in the frame of t
+        pllm::rot_q(1u - full.nq1, full.fbI, full.fbQ);
+        st[ch].feedbackI = full.fbI;
+        st[ch].feedbackQ = full.fbQ;
+        st[ch].integrator = full.ip.x;
+        st[ch].phaseEst = full.ip.y;
+        st[ch].trigOffset = full.toff;
+    }
+}
+
 // VEC: x / rx rows and the t buffer are 16-byte aligned with strides that are multiples of 4
 // (x, t) and 2 (rx), so a chunk's inputs are prefetched with 16-byte loads and the 16 phases are
 // stored with 16-byte stores -- the unrolled chunk itself touches no memory.
 // Dynamic LDS: n doubles when the launch allows the trigArg table (launch_plls), else none.
-template <bool VEC>
+// SPLIT: two lanes per channel (pll_run_split), else one.
+template <bool VEC, bool SPLIT>
 __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, int tab_ok) {
     extern __shared__ double wtab[];
-    const int ch = blockIdx.x * blockDim.x + threadIdx.x;   // lane 0 always holds a channel
+    const int lg = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = SPLIT ? lg >> 1 : lg;                    // lane 0 always holds a channel
     const bool active = ch < nch;
     const PllJob& jb = jobs.j[blockIdx.y];
     // the serial PLL bounds every block-step: let its waves win issue arbitration on shared SIMDs
@@ -455,8 +726,13 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
         __syncthreads();
     }
     if (!active) return;
-    if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
-    else pll_run<VEC, false>(jb, n, ch, nullptr);
+    if (SPLIT) {
+        if (tab) pll_run_split<VEC, true>(jb, n, ch, wtab);
+        else pll_run_split<VEC, false>(jb, n, ch, nullptr);
+    } else {
+        if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
+        else pll_run<VEC, false>(jb, n, ch, nullptr);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -475,14 +751,15 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
 // ------------------------------------------------------------------------------------------
 constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrealtime
 
-template <bool VEC>
+template <bool VEC, bool SPLIT>
 __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
                                                   const uint32_t* pre_flag, uint32_t pre_first,
                                                   uint32_t* done_ring, uint32_t* err,
                                                   unsigned long long* t_start, unsigned long long* t_end,
                                                   unsigned long long* t_cyc, int sys_acquire) {
     extern __shared__ double wtab[];
-    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lg = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = SPLIT ? lg >> 1 : lg;
     const bool active = ch < nch;
     __builtin_amdgcn_s_setprio(3);
     bool dead = false;
@@ -518,8 +795,13 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
                 __syncthreads();
             }
             if (active) {
-                if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
-                else pll_run<VEC, false>(jb, n, ch, nullptr);
+                if (SPLIT) {
+                    if (tab) pll_run_split<VEC, true>(jb, n, ch, wtab);
+                    else pll_run_split<VEC, false>(jb, n, ch, nullptr);
+                } else {
+                    if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
+                    else pll_run<VEC, false>(jb, n, ch, nullptr);
+                }
             }
             __syncthreads();   // every lane's table reads and state/phase stores issued before the release
         }
@@ -652,6 +934,15 @@ bool pll_libm_env() {
 }
 
 namespace {
+// SDR_PLL_SPLIT=0: one lane per channel even where the producer wrote -x (A/B of the lane pairs)
+bool pll_nosplit_env() {
+    static const bool v = [] {
+        const char* e = std::getenv("SDR_PLL_SPLIT");
+        return e && std::strcmp(e, "0") == 0;
+    }();
+    return v;
+}
+
 // SDR_PLL_TAB=0: per-lane trigArg offsets (A/B of the LDS table)
 bool pll_notab_env() {
     static const bool v = [] {
@@ -672,14 +963,16 @@ int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
 }
 
 int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s, bool with_nco) {
-    const dim3 g(cdiv(nch, 64), njobs), b(64);
-    bool vec = true;
+    bool vec = true, split = !pll_nosplit_env();
     for (int k = 0; k < njobs; k++) {
         const PllJob& j = jobs.j[k];
         vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
               (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
-              (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0);
+              (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0) &&
+              (!j.in_neg || reinterpret_cast<uintptr_t>(j.in_neg) % 16 == 0);
+        split = split && j.in_neg;   // lane pairs need the producer's -x row
     }
+    const dim3 g(cdiv(split ? 2 * nch : nch, 64), njobs), b(64);
     // LDS table of w * trigOffset (k_pll): n doubles, 16-byte rows
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
     const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
@@ -687,9 +980,11 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
     if (libm || pll_libm_env()) {
         hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, jobs, n, nch);
     } else if (vec) {
-        hipLaunchKernelGGL(k_pll<true>, g, b, lds, s, jobs, n, nch, tab_ok);
+        if (split) hipLaunchKernelGGL((k_pll<true, true>), g, b, lds, s, jobs, n, nch, tab_ok);
+        else hipLaunchKernelGGL((k_pll<true, false>), g, b, lds, s, jobs, n, nch, tab_ok);
     } else {
-        hipLaunchKernelGGL(k_pll<false>, g, b, lds, s, jobs, n, nch, tab_ok);
+        if (split) hipLaunchKernelGGL((k_pll<false, true>), g, b, lds, s, jobs, n, nch, tab_ok);
+        else hipLaunchKernelGGL((k_pll<false, false>), g, b, lds, s, jobs, n, nch, tab_ok);
     }
     LAUNCH_CHECK();
     return with_nco ? launch_nco(jobs, njobs, n, nch, s) : SDR_OK;
@@ -704,33 +999,35 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
     }
     PllJobs jobs{};
     jobs.j[0] = PllJob{in, in_stride, tbuf, t_stride, out, out_stride, st, freq, Fs, bw, ncoScale, phaseAdjust, nullptr,
-                       rxbuf, t_stride};
+                       rxbuf, t_stride, nullptr};
     return launch_plls(libm, jobs, 1, n, nch, s);
 }
 
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
                      hipStream_t s) {
-    bool vec = true;
+    bool vec = true, split = !pll_nosplit_env();
     for (int k = 0; k < 2; k++)
         for (int q = 0; q < 2; q++) {
             const PllJob& j = jobs.p[k].j[q];
             vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
                   (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
-                  (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0);
+                  (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0) &&
+                  (!j.in_neg || reinterpret_cast<uintptr_t>(j.in_neg) % 16 == 0);
+            split = split && j.in_neg;
         }
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
     const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
-    const dim3 g(cdiv(nch, 64), 2), b(64);
+    const dim3 g(cdiv(split ? 2 * nch : nch, 64), 2), b(64);
     *waves = g.x * g.y;
     const char* acq = std::getenv("SDR_PLL_ACQUIRE");   // diagnosis: system-scope acquire
     const int sys_acq = (acq && std::strcmp(acq, "system") == 0) ? 1 : 0;
-    if (vec)
-        hipLaunchKernelGGL(k_pll_multi<true>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
-                           words, pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc, sys_acq);
-    else
-        hipLaunchKernelGGL(k_pll_multi<false>, g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks,
-                           words, pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc, sys_acq);
+#define KPM(V, SP)                                                                                       \
+    hipLaunchKernelGGL((k_pll_multi<V, SP>), g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks, words, \
+                       pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc, sys_acq)
+    if (vec) { if (split) KPM(true, true); else KPM(true, false); }
+    else { if (split) KPM(false, true); else KPM(false, false); }
+#undef KPM
     LAUNCH_CHECK();
     return SDR_OK;
 }
