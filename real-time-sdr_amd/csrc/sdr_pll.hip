@@ -481,8 +481,13 @@ __device__ __forceinline__ SplitLane split_lane() {
 }
 
 // value of the other lane of the pair (DPP quad_perm [1,0,3,2])
+// (bound_ctrl set: both lanes of a pair are always active, and it lets the compiler fold the move
+// into the consumer as a DPP source, v_mul_f32_dpp)
+#ifndef SDR_PLL_DPP_BC
+#define SDR_PLL_DPP_BC 1
+#endif
 __device__ __forceinline__ float pair_swap(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, SDR_PLL_DPP_BC));
 }
 __device__ __forceinline__ double pair_swap(double v) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
@@ -525,12 +530,22 @@ __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx
     // pll.cpp:36-39 across the pair (see above)
     const float g = xs * pair_swap(r.fb);
     const double q = (double)g * r.f;
-    const double Y = q + pair_swap(q);
     const double base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
+#if SDR_PLL_SPLIT_ED
+    // ed = base + rx qA + rx qB with the own product first: one dependent level less after q, but
+    // the two lanes round in different orders, so each lane proves both ends of its own bracket
+    const double ed = pllm::fma_(pair_swap(q), rx, pllm::fma_(q, rx, base));
+    const float e = (float)ed;
+    pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, (float)(ed - pllm::EPS_ABS_E2)),
+                      __builtin_bit_cast(uint32_t, (float)(ed + pllm::EPS_ABS_E2)));
+    (void)L;
+#else
+    const double Y = q + pair_swap(q);
     const double ed = pllm::fma_(Y, rx, base);
     const float e = (float)ed;                                     // = RN32(atan2) when proven
-    pf.emaxf = fmaxf(pf.emaxf, __builtin_fabsf(e));               // f32: two steps per v_max3_f32
     pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, (float)(ed + L.eps)), __builtin_bit_cast(uint32_t, e));
+#endif
+    pf.emaxf = fmaxf(pf.emaxf, __builtin_fabsf(e));               // f32: two steps per v_max3_f32
     {   // pll.cpp:41-42
         const float ki_e = Ki * e;
         const float integ = r.ip.x + ki_e;
