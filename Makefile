@@ -32,8 +32,11 @@ lib: $(LIB)
 host: $(HOSTLIB) $(CLI) $(MULTI)
 
 # one object per translation unit (compiled in parallel), linked into the shared library
-# the stage kernels keep their f32 multiply-adds scalar (packed f32 runs at half rate): no SLP
+# the stage kernels keep their f32 multiply-adds scalar (packed f32 runs at half rate): no SLP;
+# the lane-pair PLL step is faster scalar too (packed-f32 results cost a wait state on gfx950,
+# profiles/r03/ab_pll_split3.txt)
 build/sdr_kernels.hip.o: HIPFLAGS += -fno-slp-vectorize
+build/sdr_pll.hip.o: HIPFLAGS += -fno-slp-vectorize
 
 build/%.o: $(PKG)/csrc/% $(HDRS)
 	@mkdir -p build

@@ -310,8 +310,10 @@ class GpuStepper:
             "pll": {"kernel": ("k_pll_multi: persistent, all blocks of the phase in one dispatch" if self.persist
                                else "k_pll: one dispatch per block") +
                               ", stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial chains",
-                    "bound": "serial recurrence: block_if dependent steps per chain, one lane per chain "
-                             "(per-wave VALU issue, DESIGN.md 4a)",
+                    "bound": "serial recurrence: block_if dependent steps per chain, " +
+                             ("one lane per chain" if os.environ.get("SDR_PLL_SPLIT") == "0"
+                              else "a lane pair per chain (cos / sin lanes)") +
+                             " (per-wave issue and dependent latency, DESIGN.md 4a)",
                     "mode": self.pll_mode,
                     "avg_launch_ms": round(pll_ms, 4), "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
                     "share_of_step": round(pll_ms / (elapsed / steps * 1e3), 4),

@@ -72,8 +72,10 @@ struct PllJob {
     // pll_math.h pll_rx of every input sample (written by the producer of `in`)
     const double* rx;
     size_t rx_stride;
-    // -in, same layout (written by the producer): with it the PLL runs on lane pairs (sdr_pll.hip)
+    // -in (written by the producer; row stride neg_stride): with it the PLL runs on lane pairs
+    // (sdr_pll.hip pll_run_split)
     const float* in_neg;
+    size_t neg_stride;
 };
 struct PllJobs {
     PllJob j[2];
@@ -110,9 +112,10 @@ bool pll_libm_env();
 int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s);
 int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s, bool with_nco = true);
 // the context-free fmpll primitive: reciprocals, PLL, NCO
+// (tbuf, rxbuf, negbuf: scratch [nch][t_stride]; negbuf receives -in for the lane-pair PLL)
 int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
-               size_t t_stride, double* rxbuf, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale,
-               float phaseAdjust, float bw, hipStream_t s);
+               size_t t_stride, double* rxbuf, float* negbuf, float* out, size_t out_stride, sdr_pll_state* st,
+               float ncoScale, float phaseAdjust, float bw, hipStream_t s);
 // persistent PLLs: words = [pre_flag, err, (pad), (pad), done ring of PLL_DONE_RING per-sequence
 // counters]; returns the number of waves in *waves. Block sequence s is done when its ring slot
 // done[s % PLL_DONE_RING] reaches waves * (s / PLL_DONE_RING + 1): per-block counters, because

@@ -1196,14 +1196,14 @@ PllJob stereo_job(sdr_ctx* c) {   // stereo.cpp:77: fmpll(pilot, 19e3, rf_Fs/rf_
     return PllJob{c->plain(c->pilot), c->plain_stride, c->plain(c->t_st), c->plain_stride, c->pllbuf(c->carrier),
                   c->pll_stride, c->st_pll, 19e3f, (float)(in.rf_Fs / in.rf_decim), 0.01f, 2.0f, 0.0f,
                   c->carrier + (c->parity ^ 1) * c->pll_par, c->rxbuf(c->rx_st), c->plain_stride,
-                  c->plain(c->pilot_neg)};
+                  c->plain(c->pilot_neg), c->plain_stride};
 }
 PllJob rds_job(sdr_ctx* c) {      // rds.cpp:119: fmpll(gen_pilot, 114e3, if_Fs, ..., 0.5, 0, 0.001)
     const sdr_info& in = c->info;
     return PllJob{c->plain(c->gpilot), c->plain_stride, c->plain(c->t_rds), c->plain_stride, c->pllbuf(c->ipll),
                   c->pll_stride, c->rds_pll, 114e3f, (float)in.if_Fs, 0.001f, 0.5f, 0.0f,
                   c->ipll + (c->parity ^ 1) * c->pll_par, c->rxbuf(c->rx_rds), c->plain_stride,
-                  c->plain(c->gpilot_neg)};
+                  c->plain(c->gpilot_neg), c->plain_stride};
 }
 
 }  // namespace
@@ -2180,7 +2180,8 @@ int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, 
               sdr_pll_state* state, float ncoScale, float phaseAdjust, float normBandwidth, void* stream) {
     if (!out || !in || !state || nch <= 0 || n < 0) return fail(SDR_E_INVALID, "fmpll: bad arguments");
     const size_t ts = round_up((size_t)std::max(n, 1), 4);
-    const size_t rx_bytes = ts * nch * sizeof(double), t_bytes = ts * nch * sizeof(float);
+    // scratch: input reciprocals (f64), phases and -in (f32), each [nch][ts]
+    const size_t rx_bytes = ts * nch * sizeof(double), t_bytes = 2 * ts * nch * sizeof(float);
     const int mode = fmpll_scratch_mode();
     hipStream_t s = S(stream);
     if (mode >= 2) {
@@ -2189,8 +2190,8 @@ int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, 
         HIP_TRY(hipMallocAsync(&tp, t_bytes, s));
         if (mode == 4) HIP_TRY(hipStreamSynchronize(s));
         const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, static_cast<float*>(tp), ts,
-                                 static_cast<double*>(rxp), out, out_stride, state, ncoScale, phaseAdjust,
-                                 normBandwidth, s);
+                                 static_cast<double*>(rxp), static_cast<float*>(tp) + ts * nch, out, out_stride,
+                                 state, ncoScale, phaseAdjust, normBandwidth, s);
         if (mode != 3) {
             HIP_TRY(hipFreeAsync(rxp, s));
             HIP_TRY(hipFreeAsync(tp, s));
@@ -2208,8 +2209,8 @@ int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, 
     }
     double* rxbuf = static_cast<double*>(scratch);
     float* tbuf = reinterpret_cast<float*>(rxbuf + ts * nch);
-    const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, tbuf, ts, rxbuf, out, out_stride, state, ncoScale,
-                             phaseAdjust, normBandwidth, s);
+    const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, tbuf, ts, rxbuf, tbuf + ts * nch, out, out_stride,
+                             state, ncoScale, phaseAdjust, normBandwidth, s);
     if (mode == 1) {
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(hipFree(scratch));

@@ -547,9 +547,14 @@ __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx
 #endif
     pf.emaxf = fmaxf(pf.emaxf, __builtin_fabsf(e));               // f32: two steps per v_max3_f32
     {   // pll.cpp:41-42
-        const float ki_e = Ki * e;
+        float ki_e = Ki * e, kp_e = Kp * e;
+#if SDR_PLL_SPLIT_LF
+        // scalar f32 (5 instructions): the SLP-packed form reads packed-f32 results, and on gfx950 each
+        // such read waits a state (s_nop) on the step's dependent chain
+        asm("" : "+v"(ki_e), "+v"(kp_e));
+#endif
         const float integ = r.ip.x + ki_e;
-        r.ip.y = (r.ip.y + Kp * e) + integ;
+        r.ip.y = (r.ip.y + kp_e) + integ;
         r.ip.x = integ;
     }
     float t;
@@ -568,10 +573,30 @@ __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx
     r.b = (uint32_t)(__builtin_bit_cast(uint64_t, rr) >> 63);
     r.mr = -rr;
     const double z = rr * rr, z2 = z * z;
+    const double u = pllm::fma_(rr, L.k1, L.k0);
+#ifndef SDR_PLL_SPLIT_POLY
+#define SDR_PLL_SPLIT_POLY 1   // Horner (profiles/r03/ab_pll_split3.txt)
+#endif
+#if SDR_PLL_SPLIT_POLY == 2
+    // f = (u + zu A01) + zu z^2 (A23 + z^2 A45): one multiply more, one dependent level less
+    const double zu = z * u;
+    const double B = pllm::fma_(z2, pllm::fma_(z, L.c5, L.c4), pllm::fma_(z, L.c3, L.c2));
+    const double Cl = pllm::fma_(zu, pllm::fma_(z, L.c1, L.c0), u);
+    r.f = pllm::fma_(zu * z2, B, Cl);
+#elif SDR_PLL_SPLIT_POLY == 1
+    // Horner: one instruction fewer than Estrin (no z^2), two dependent levels more
+    (void)z2;
+    double P = pllm::fma_(z, L.c5, L.c4);
+    P = pllm::fma_(z, P, L.c3);
+    P = pllm::fma_(z, P, L.c2);
+    P = pllm::fma_(z, P, L.c1);
+    P = pllm::fma_(z, P, L.c0);
+    r.f = pllm::fma_(z * u, P, u);
+#else
     const double P = pllm::fma_(z2, pllm::fma_(z2, pllm::fma_(z, L.c5, L.c4), pllm::fma_(z, L.c3, L.c2)),
                                 pllm::fma_(z, L.c1, L.c0));
-    const double u = pllm::fma_(rr, L.k1, L.k0);
     r.f = pllm::fma_(z * u, P, u);
+#endif
     r.fb = (float)r.f;                                             // pll.cpp:49-50, reduced frame
     pf.tie = min(pf.tie, pllm::tie_key64(r.f));                   // this lane's rounding (pll_math.h)
     if (!TAB) pf.tmax = fmaxf(pf.tmax, __builtin_fabsf(t));
@@ -592,7 +617,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
     const double w = 2 * 3.14159265358979323846 * (freq / Fs);
     const sdr_pll_state s0 = st[ch];
     const float* xpos = jb.in + (size_t)ch * in_stride;
-    const float* xs = (L.a ? jb.in_neg : jb.in) + (size_t)ch * in_stride;   // lane A: -x
+    const float* xs = L.a ? jb.in_neg + (size_t)ch * jb.neg_stride : xpos;   // lane A: -x
     const double* rxp = jb.rx + (size_t)ch * jb.rx_stride;
     float* tb = jb.tbuf + (size_t)ch * t_stride;
     if (!jb.prev_out && L.a) jb.out[(size_t)ch * out_stride] = s0.lastCarrier;   // pll.cpp:18
@@ -855,12 +880,16 @@ __global__ void k_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err) {
     }
 }
 
-// pll_rx of a PLL input with no fused producer (the batched sdr_fmpll primitive)
-__global__ __launch_bounds__(BLK) void k_pll_rx(double* __restrict__ rx, size_t rx_stride, const float* __restrict__ x,
-                                                size_t x_stride, int n) {
+// pll_rx and -x of a PLL input with no fused producer (the batched sdr_fmpll primitive)
+__global__ __launch_bounds__(BLK) void k_pll_rx(double* __restrict__ rx, float* __restrict__ xneg, size_t rx_stride,
+                                                const float* __restrict__ x, size_t x_stride, int n) {
     const int ch = blockIdx.y;
     const int i = blockIdx.x * BLK + threadIdx.x;
-    if (i < n) rx[(size_t)ch * rx_stride + i] = pllm::pll_rx(x[(size_t)ch * x_stride + i]);
+    if (i < n) {
+        const float v = x[(size_t)ch * x_stride + i];
+        rx[(size_t)ch * rx_stride + i] = pllm::pll_rx(v);
+        xneg[(size_t)ch * rx_stride + i] = -v;
+    }
 }
 
 __global__ __launch_bounds__(64) void k_pll_libm(const PllJobs jobs, int n, int nch) {
@@ -984,7 +1013,7 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
         vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
               (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
               (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0) &&
-              (!j.in_neg || reinterpret_cast<uintptr_t>(j.in_neg) % 16 == 0);
+              (!j.in_neg || (reinterpret_cast<uintptr_t>(j.in_neg) % 16 == 0 && j.neg_stride % 4 == 0));
         split = split && j.in_neg;   // lane pairs need the producer's -x row
     }
     const dim3 g(cdiv(split ? 2 * nch : nch, 64), njobs), b(64);
@@ -1006,15 +1035,16 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
 }
 
 int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, float freq, float Fs, float* tbuf,
-               size_t t_stride, double* rxbuf, float* out, size_t out_stride, sdr_pll_state* st, float ncoScale,
-               float phaseAdjust, float bw, hipStream_t s) {
+               size_t t_stride, double* rxbuf, float* negbuf, float* out, size_t out_stride, sdr_pll_state* st,
+               float ncoScale, float phaseAdjust, float bw, hipStream_t s) {
     if (n > 0) {
-        hipLaunchKernelGGL(k_pll_rx, dim3(cdiv(n, BLK), nch), dim3(BLK), 0, s, rxbuf, t_stride, in, in_stride, n);
+        hipLaunchKernelGGL(k_pll_rx, dim3(cdiv(n, BLK), nch), dim3(BLK), 0, s, rxbuf, negbuf, t_stride, in, in_stride,
+                           n);
         LAUNCH_CHECK();
     }
     PllJobs jobs{};
     jobs.j[0] = PllJob{in, in_stride, tbuf, t_stride, out, out_stride, st, freq, Fs, bw, ncoScale, phaseAdjust, nullptr,
-                       rxbuf, t_stride, nullptr};
+                       rxbuf, t_stride, negbuf, t_stride};
     return launch_plls(libm, jobs, 1, n, nch, s);
 }
 
@@ -1028,7 +1058,7 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
             vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
                   (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
                   (reinterpret_cast<uintptr_t>(j.rx) % 16 == 0) && (j.rx_stride % 2 == 0) &&
-                  (!j.in_neg || reinterpret_cast<uintptr_t>(j.in_neg) % 16 == 0);
+                  (!j.in_neg || (reinterpret_cast<uintptr_t>(j.in_neg) % 16 == 0 && j.neg_stride % 4 == 0));
             split = split && j.in_neg;
         }
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);

@@ -1,10 +1,18 @@
-# Build a variant of libsdr_amd.so with extra -D flags into build/variants/<name>.so, for A/B timing
-# through SDR_AMD_LIB=<path> (tools/gpu/*.sh). Usage: bash tools/build_variant.sh <name> -DFOO=1 ...
+# Build a variant of libsdr_amd.so with extra flags into build/variants/<name>.so, for A/B timing
+# through SDR_AMD_LIB=<path> (tools/gpu/*.sh); per-file flags as in the Makefile.
+#   bash tools/build_variant.sh <name> -DFOO=1 ...
 set -e
 name=$1; shift
-mkdir -p build/variants
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-flush-denormals-to-zero \
-  -mllvm -pragma-unroll-threshold=1000000 -Iinclude "$@" -shared -Wl,-soname,libsdr_amd.so \
-  -o build/variants/$name.so real-time-sdr_amd/csrc/sdr_kernels.hip real-time-sdr_amd/csrc/sdr_frontend.hip \
-  real-time-sdr_amd/csrc/sdr_pll.hip real-time-sdr_amd/csrc/sdr_taps.cpp
+d=build/variants/$name.obj
+mkdir -p $d
+common="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-flush-denormals-to-zero -mllvm -pragma-unroll-threshold=1000000 -Iinclude"
+pids=""
+for f in sdr_kernels.hip sdr_frontend.hip sdr_pll.hip sdr_taps.cpp; do
+  extra=""
+  case $f in sdr_kernels.hip|sdr_pll.hip) extra=-fno-slp-vectorize;; esac
+  /opt/rocm/bin/hipcc $common $extra "$@" -c -o $d/$f.o real-time-sdr_amd/csrc/$f & pids="$pids $!"
+done
+for p in $pids; do wait $p; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -Wl,-soname,libsdr_amd.so -o build/variants/$name.so $d/*.o
+rm -rf $d
 echo build/variants/$name.so

@@ -56,6 +56,14 @@ CHAIN(i_mix_f64_f32, double, "v_fma_f64 %0, %0, %4, %4\n v_xor_b32 %5, %5, %5\n 
       "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "v"(a), "v"(0), "v"(1))
 CHAIN(i_mov_dpp, float, "v_mov_b32_dpp %0, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n v_mov_b32_dpp %1, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n v_mov_b32_dpp %2, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n v_mov_b32_dpp %3, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf",
       "=v"(x), "=v"(y), "=v"(z), "=v"(w) : "v"(a))
+// the DPP exchange on the lane-pair PLL's chain: a DPP read of a VGPR written by the previous VALU
+// instruction needs 2 wait states (s_nop 1 here, as the compiler inserts)
+CHAIN(d_mov_dpp, float, "s_nop 1\n v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf", "+v"(x))
+CHAIN(d_mul_dpp, float, "s_nop 1\n v_mul_f32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1",
+      "+v"(x) : "v"(a))
+CHAIN(d_nop_mul, float, "s_nop 1\n v_mul_f32 %0, %0, %1", "+v"(x) : "v"(a))
+CHAIN(d_pk_mul, double, "v_pk_mul_f32 %0, %0, %1", "+v"(x) : "v"(a))
+CHAIN(d_cvt_f64_f32, float, "v_cvt_f64_f32 v[40:41], %0\n v_cvt_f32_f64 %0, v[40:41]", "+v"(x) : : "v40", "v41")
 CHAIN(d_cvt_rt, float, "v_cvt_f64_f32 v[40:41], %0\n v_cvt_f32_f64 %0, v[40:41]", "+v"(x) : : "v40", "v41")
 
 template <typename TY>
@@ -100,5 +108,9 @@ int main() {
     run(i_mix_f64_f32, "ind fma64+xor", 4);
     run(i_mov_dpp, "ind mov_dpp", 4);
     run(d_cvt_rt, "dep cvt 64<-32->", 2);
+    run(d_mov_dpp, "dep nop1+mov_dpp", 1);
+    run(d_mul_dpp, "dep nop1+mul_dpp", 1);
+    run(d_nop_mul, "dep nop1+mul_f32", 1);
+    run(d_pk_mul, "dep pk_mul", 1);
     return 0;
 }
