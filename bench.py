@@ -195,7 +195,8 @@ class GpuStepper:
         tev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
         self.fe_start, self.fe_end = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
         self.pll_start, self.pll_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
-        self.pre_done, self.post_done, self.gather_done = ([ev() for _ in range(nblocks)] for _ in range(3))
+        self.gather_done = [ev() for _ in range(nblocks)]
+        self.pre_done, self.post_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
         # outputs of a few channels, captured on the producing streams for the check after timing
         nv = min(VERIFY_CHANNELS, nch)
         self.vsel = torch.tensor(sorted({int(round(i * (nch - 1) / max(1, nv - 1))) for i in range(nv)}),
@@ -232,6 +233,7 @@ class GpuStepper:
         pipe.pre(stream=s_fe)                                 # stereo.cpp:74, :80 + rds.cpp:105-116
         if self.persist:                                      # stereo.cpp:77 + rds.cpp:119
             pipe.plls_signal(stream=s_fe)
+            self.pre_done[b].record(s_fe)
             pipe.plls_wait(stream=s_post)
         else:
             self.pre_done[b].record(s_fe)
@@ -294,9 +296,26 @@ class GpuStepper:
         fe_avg_s = float(np.mean([self.fe_start[b].elapsed_time(self.fe_end[b]) for b in rng])) / 1e3
         fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
         cyc = None
+        timeline = None
         if self.persist:   # device-clock time of each block inside the timed phase's dispatch
             pll_ms = float(np.mean(self.pipe.plls_report(stream=self.s_pll)))
             cyc = self.pipe.plls_cycles(stream=self.s_pll)   # the waves' own shader-clock count
+            ts, te = self.pipe.plls_timeline(stream=self.s_pll)
+            if ts and te:
+                # the timed phase on the device clock: the PLL span from block 0's signal to the last
+                # block's end, the PLL's idle time between blocks (input not ready), and what the
+                # host-timed phase spends outside the span (pipeline fill before block 0's PLL and
+                # the last block's post stage after it)
+                span = (te[-1] - ts[0]) * 1e-5
+                idle = sum(max(0, ts[j] - te[j - 1]) for j in range(1, len(ts))) * 1e-5
+                first, last = warmup, warmup + steps - 1
+                phase = self.fe_start[first].elapsed_time(self.post_done[last])
+                fill = self.fe_start[first].elapsed_time(self.pre_done[first])
+                timeline = {"pll_span_ms": round(span, 4), "pll_idle_ms": round(idle, 4),
+                            "outside_span_ms": round(elapsed * 1e3 - span, 4),
+                            "device_phase_ms": round(phase, 4), "fill_ms": round(fill, 4),
+                            "fill_frontend_ms": round(self.fe_start[first].elapsed_time(self.fe_end[first]), 4),
+                            "drain_ms": round(phase - fill - span, 4)}
         else:
             pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
         achieved = fe_bytes / fe_avg_s / 1e9
@@ -318,6 +337,7 @@ class GpuStepper:
                     "avg_launch_ms": round(pll_ms, 4), "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
                     "share_of_step": round(pll_ms / (elapsed / steps * 1e3), 4),
                     **self._pll_issue(cyc),
+                    **({"timeline": timeline} if timeline else {}),
                     **({"chunk_redo": redo} if redo else {})},
         }
 
@@ -498,6 +518,7 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
             st.begin_phase(args.steps)
         for b in range(args.warmup, nblocks):
             st.step(b, gather)
+        t_enq = time.perf_counter() - t0          # host time to enqueue the K block-steps
         st.synchronize()
         if world > 1:
             dist.barrier()
@@ -537,6 +558,7 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
                 "steps": args.steps,
                 "warmup": args.warmup,
                 "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
                 "higher_is_better": True,
                 "scaling": "weak",
                 "vs_baseline": None,

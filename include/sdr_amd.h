@@ -170,6 +170,10 @@ int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
 int sdr_plls_signal(sdr_ctx *ctx, void *stream);
 int sdr_plls_wait(sdr_ctx *ctx, void *stream);
 int sdr_plls_report(sdr_ctx *ctx, double *block_ms, int max_blocks, int *nblocks, void *stream);
+/* The raw device stamps of the last persistent launch (100 MHz s_memrealtime ticks), per block:
+ * t_start[j] = when its signal was seen, t_end[j] = its last wave's end; synchronises `stream`. */
+int sdr_plls_timeline(sdr_ctx *ctx, unsigned long long *t_start, unsigned long long *t_end, int max_blocks,
+                      int *nblocks, void *stream);
 /* Per-step cost of the last persistent launch from the waves' own clocks: shader cycles per PLL step
  * and wave (s_memtime over each wave's compute of each block, averaged) and the shader clock over
  * the same intervals (against the 100 MHz s_memrealtime); synchronises `stream`. */

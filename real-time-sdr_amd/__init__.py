@@ -94,6 +94,7 @@ def lib() -> C.CDLL:
         "sdr_plls_wait": ([vp, vp], i32),
         "sdr_plls_report": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32), vp], i32),
         "sdr_plls_cycles": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), vp], i32),
+        "sdr_plls_timeline": ([vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), i32, C.POINTER(i32), vp], i32),
         "sdr_rds_post": ([vp, vp, sz, vp], i32),
         "sdr_ctx_buffer": ([vp, C.c_char_p, C.POINTER(vp), C.POINTER(sz), C.POINTER(i32)], i32),
         "sdr_hbm_copy": ([vp, vp, sz, vp], i32),
@@ -338,6 +339,13 @@ class Pipeline:
         n = C.c_int(0)
         check(lib().sdr_plls_report(self._h, arr, max_blocks, C.byref(n), _stream(stream)), "sdr_plls_report")
         return list(arr[:n.value])
+
+    def plls_timeline(self, max_blocks: int = 4096, stream=None) -> tuple[list, list]:
+        """(t_start, t_end) per block of the last persistent launch, 100 MHz device ticks."""
+        a, z = (C.c_ulonglong * max_blocks)(), (C.c_ulonglong * max_blocks)()
+        n = C.c_int(0)
+        check(lib().sdr_plls_timeline(self._h, a, z, max_blocks, C.byref(n), _stream(stream)), "sdr_plls_timeline")
+        return list(a[:n.value]), list(z[:n.value])
 
     def plls_cycles(self, stream=None) -> tuple[float, float]:
         """(shader cycles per PLL step and wave, shader clock MHz) of the last persistent launch."""

@@ -1937,6 +1937,20 @@ int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, 
     return SDR_OK;
 }
 
+int sdr_plls_timeline(sdr_ctx* c, unsigned long long* t_start, unsigned long long* t_end, int max_blocks, int* nblocks,
+                      void* stream) {
+    if (!c || !c->pers_words) return fail(SDR_E_INVALID, "plls_timeline: no persistent launch");
+    hipStream_t s = S(stream);
+    const int n = std::min(c->pers_last_n, std::max(max_blocks, 0));
+    if (n > 0 && t_start)
+        HIP_TRY(hipMemcpyAsync(t_start, c->pers_t0, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if (n > 0 && t_end)
+        HIP_TRY(hipMemcpyAsync(t_end, c->pers_t1, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (nblocks) *nblocks = n;
+    return SDR_OK;
+}
+
 int sdr_plls_cycles(sdr_ctx* c, double* cycles_per_step, double* clock_mhz, void* stream) {
     if (!c || !c->pers_cyc || c->pers_last_n <= 0) return fail(SDR_E_INVALID, "plls_cycles: no persistent launch");
     hipStream_t s = S(stream);

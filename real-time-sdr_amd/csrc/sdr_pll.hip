@@ -808,8 +808,11 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
         if (!dead) {
             const uint32_t want = pre_first + (uint32_t)j + 1u;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while ((int32_t)((sys_acquire ? __hip_atomic_load(pre_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)
-                                          : __hip_atomic_load(pre_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) -
+            // poll with relaxed loads and acquire once: an acquire load at agent scope invalidates
+            // the wave's caches (on a multi-XCD device its XCD's L2) on every poll, which slowed the
+            // kernels running beside the waiting waves 2-3x
+            while ((int32_t)((sys_acquire ? __hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : __hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
                              want) < 0) {
                 __builtin_amdgcn_s_sleep(4);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
@@ -817,6 +820,10 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
                     break;
                 }
             }
+            if (sys_acquire)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            else
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             if (dead && threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         unsigned long long c0 = 0, r0 = 0;   // this wave's shader-clock and 100 MHz stamps of the block
@@ -871,13 +878,14 @@ __global__ void k_flag_store(uint32_t* flag, uint32_t v) {
 __global__ void k_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err) {
     if (threadIdx.x != 0) return;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int32_t)(__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+    while ((int32_t)(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
         __builtin_amdgcn_s_sleep(4);
         if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
             __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // once, after the poll (see k_pll_multi)
 }
 
 // pll_rx and -x of a PLL input with no fused producer (the batched sdr_fmpll primitive)
