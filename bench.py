@@ -82,19 +82,23 @@ def launch_ranks(args, argv: list[str]) -> int:
 
 # ------------------------------------------------------------------------------ GPU stepper
 def cu_masked_streams(torch, pkg, dev, spec: str, created: list):
-    """(fe, pll, post) streams on disjoint CUs through the C ABI (sdr_stream_create_cu_range):
-    the PLL stream on CUs [0, n), the other two on the rest. The runtime creates these streams
-    blocking (hipExtStreamCreateWithCUMask has no flags), so nothing in the timed loop may run on
-    the legacy null stream: the RCCL gather gets its own non-blocking torch stream."""
+    """(fe, pll, post, all) streams through the C ABI (sdr_stream_create_cu_range): the PLL stream
+    on CUs [0, n), front end and post on the rest, and one stream over every CU for the pipeline's
+    fill and drain (the first block's pre-PLL work and the last block's post-PLL work, when the PLL
+    CUs have nothing else to do). Every masked stream gets its own hardware queue. The runtime
+    creates these streams blocking (hipExtStreamCreateWithCUMask has no flags), so nothing in the
+    timed loop may run on the legacy null stream: the RCCL gather gets its own non-blocking torch
+    stream."""
     import ctypes as C
     n = int(spec)
     L = pkg.lib()
     L.sdr_stream_create_cu_range.restype = C.c_int
     L.sdr_stream_create_cu_range.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int]
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     out = []
-    for exclude in (1, 0, 1):
+    for lo, hi, exclude in ((0, n, 1), (0, n, 0), (0, n, 1), (0, ncu, 0)):
         h = C.c_void_p()
-        rc = L.sdr_stream_create_cu_range(C.byref(h), dev.index, 0, n, exclude)
+        rc = L.sdr_stream_create_cu_range(C.byref(h), dev.index, lo, hi, exclude)
         if rc != 0:
             raise RuntimeError(f"sdr_stream_create_cu_range: {rc} {L.sdr_last_error()}")
         created.append(h.value)
@@ -160,6 +164,7 @@ class GpuStepper:
         prio = set(filter(None, os.environ.get("SDR_BENCH_PRIO", "").split(",")))
         s_fe, s_pll, s_post = (torch.cuda.Stream(dev, priority=-1 if n in prio else 0)
                                for n in ("fe", "pll", "post"))
+        s_all = None
         # SDR_BENCH_CUMASK=<n> (default 64; 0 = no masks): the PLL stream gets CUs [0, n), the
         # front-end and post streams the complement, so that no other kernel shares a CU's issue
         # slots with the PLL's lone waves (profiles/r01/ab_cumask.txt).
@@ -167,13 +172,16 @@ class GpuStepper:
         cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64")
         if cu_spec not in ("", "0"):
             try:
-                s_fe, s_pll, s_post = cu_masked_streams(torch, pkg, dev, cu_spec, self.created)
+                s_fe, s_pll, s_post, s_all = cu_masked_streams(torch, pkg, dev, cu_spec, self.created)
             except (RuntimeError, ValueError, AttributeError) as exc:   # plain streams, reported
                 print(f"bench: CU-masked streams unavailable ({exc}); unmasked streams", file=sys.stderr)
                 destroy_masked_streams(torch, pkg, dev, self.created)
                 cu_spec = ""
         self.cu_spec = cu_spec
         self.s_fe, self.s_pll, self.s_post = s_fe, s_pll, s_post
+        # SDR_BENCH_EDGES=0: the first and last block of a phase stay on their masked streams
+        self.s_all = s_all if os.environ.get("SDR_BENCH_EDGES", "1") != "0" else None
+        self.phase = (0, -1)        # first and last block index of the current phase
         # SDR_BENCH_PLL=persistent (default): one PLL dispatch per phase (warm-up, timed) that waits
         # for each block's device flag (sdr_plls_launch/_signal/_wait); "dispatch": one sdr_plls
         # dispatch per block, ordered by events. The persistent kernel's waves spin until a later
@@ -216,10 +224,25 @@ class GpuStepper:
         """Before the warm-up and before the timed blocks: the persistent PLL dispatch of the phase."""
         if self.persist:
             self.pipe.plls_launch(nblocks, stream=self.s_pll)
+        self.next_first = True
+        self.phase_len = nblocks
 
     def step(self, b: int, gather=None) -> None:
         torch, pipe = self.torch, self.pipe
         s_fe, s_pll, s_post = self.s_fe, self.s_pll, self.s_post
+        # pipeline fill and drain: nothing runs beside the first block's pre-PLL work or the last
+        # block's post-PLL work, so those take every CU (the all-CU stream), ordered by events
+        first = getattr(self, "next_first", False)
+        self.next_first = False
+        if first:
+            self.phase = (b, b + getattr(self, "phase_len", 1) - 1)
+        edge_fe = self.s_all is not None and b == self.phase[0]
+        edge_post = self.s_all is not None and b == self.phase[1]
+        if edge_fe:
+            s_fe = self.s_all
+        if edge_post:
+            s_post = self.s_all
+            s_post.wait_event(self.post_done[b - 1]) if b >= 1 else None
         # the front end of block b reuses block b-2's parity: both consumers must have released it
         # (threadsafequeue.h:29-31), i.e. block b-2's post-PLL work is done
         if b >= 2:
@@ -227,16 +250,19 @@ class GpuStepper:
         self.fe_start[b].record(s_fe)
         pipe.frontend(self.iq[b], stream=s_fe)                # rffrontend.cpp:58-71
         self.fe_end[b].record(s_fe)
-        pipe.mono(self.mono, stream=s_fe)                     # mono.cpp:34-42
-        with torch.cuda.stream(s_fe):
-            torch.index_select(self.mono, 0, self.vsel, out=self.cap_mono[b])
         pipe.pre(stream=s_fe)                                 # stereo.cpp:74, :80 + rds.cpp:105-116
         if self.persist:                                      # stereo.cpp:77 + rds.cpp:119
             pipe.plls_signal(stream=s_fe)
-            self.pre_done[b].record(s_fe)
+        self.pre_done[b].record(s_fe)
+        if edge_fe:                                           # the rest of the phase's front ends follow it
+            s_fe = self.s_fe
+            s_fe.wait_event(self.pre_done[b])
+        pipe.mono(self.mono, stream=s_fe)                     # mono.cpp:34-42 (off the PLLs' critical path)
+        with torch.cuda.stream(s_fe):
+            torch.index_select(self.mono, 0, self.vsel, out=self.cap_mono[b])
+        if self.persist:
             pipe.plls_wait(stream=s_post)
         else:
-            self.pre_done[b].record(s_fe)
             s_pll.wait_event(self.pre_done[b])
             self.pll_start[b].record(s_pll)
             pipe.plls(stream=s_pll)
@@ -749,6 +775,16 @@ def cpu_baseline_leg(args, cap: dict | None, timing: bool = True) -> dict:
                             "sample": f"{nproc} concurrent `project 0 r` processes x 3 threads, distinct channels, "
                                       f"3200 blocks each, {dt2:.2f} s wall (one GPU's CPU share)"}
         res["host_cpus"] = host
+        # the node's CPU figure by extrapolation (not measured: this job's cgroup owns `usable` CPUs):
+        # the measured rate per reference process times floor(nproc / 3) processes, i.e. the 3-thread
+        # topology (project.cpp:134-136) on every hardware thread of the host with perfect scaling
+        nproc_node = max(1, (host["nproc"] or 1) // 3)
+        res["node_extrapolated"] = {
+            "value": round(v / nproc * nproc_node, 3), "unit": "MS/s", "cores": 3 * nproc_node,
+            "kind": "reference", "measured": False,
+            "sample": f"all_cores rate per process ({v / nproc:.2f} MS/s) x {nproc_node} processes = "
+                      f"floor(nproc {host['nproc']} / 3); an upper bound (perfect scaling, no SMT or memory "
+                      f"contention) for the whole node's CPUs"}
         # the whole host (floor(usable / 3) processes) only on request: a GPU job on this pool owns a
         # 16-CPU share of the node, the other GPUs' jobs share the rest (SDR_BENCH_CPU_CORES)
         if os.environ.get("SDR_BENCH_HOST_LEG", "0") == "1":

@@ -6,6 +6,7 @@
 #include "sdr_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -111,9 +112,25 @@ __global__ __launch_bounds__(BLK) void k_frontend(
 #define SDR_FE_CVT_MID 0   // 1: conversion between the products (more hazard wait states: not adopted)
 #endif
 constexpr int FE_PF = SDR_FE_PF;   // tap rows prefetched this many samples ahead (rotating SGPR ring)
+// SDR_FE_VTAP=1: the exact front end keeps all 101 taps (h/128, 51 VGPR pairs) in registers instead
+// of streaming per-sample tap rows through SGPRs. Scalar loads return out of order, so every use of a
+// prefetched SGPR row waits for ALL scalar loads in flight (lgkmcnt(0), which the LDS window reads
+// share): the SGPR ring exposes the scalar-cache latency every few samples.
+// Not adopted: the 102 tap VGPRs leave 2 waves per SIMD and the kernel runs 8 % slower
+// (profiles/r03/ab_fe_vtap.txt).
+#ifndef SDR_FE_VTAP
+#define SDR_FE_VTAP 0
+#endif
 
 // {h, h} * m with h one half (HI) of an SGPR pair: v_pk_mul_f32 with a scalar operand whose half
 // is broadcast to both lanes by op_sel / op_sel_hi (no VGPR copy of the tap)
+// the same with the tap pair in VGPRs (SDR_FE_VTAP: all taps resident in registers)
+__device__ __forceinline__ f32x2 fe_mul_vv(double hpair, int hi, f32x2 m) {
+    f32x2 r;
+    if (hi) asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(hpair), "v"(m));
+    else asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(hpair), "v"(m));
+    return r;
+}
 __device__ __forceinline__ f32x2 fe_mul_v(double hpair, int hi, f32x2 m) {
     f32x2 r;
     if (hi) asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "s"(hpair), "v"(m));
@@ -695,7 +712,7 @@ template <int R, int D, bool FAST, bool PF>
 __global__ __launch_bounds__(64) void k_frontend2(
     const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
     uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
-    const float* __restrict__ hs, int block_iq, int block_if,
+    const float* __restrict__ hs, const float* __restrict__ hv, int block_iq, int block_if,
     float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int nch, int tiles_ch,
     const uint32_t* __restrict__ pad) {
     constexpr int NT = 101, HP = NT - 1, NTH = 64;
@@ -755,6 +772,15 @@ __global__ __launch_bounds__(64) void k_frontend2(
         }
     };
     fetch(tile);
+#if SDR_FE_VTAP
+    double tv[(NT + 1) / 2];          // tv[j] = {h[2j], h[2j+1]} / 128, uniform, held in VGPRs
+#pragma unroll
+    for (int j = 0; j < (NT + 1) / 2; j++) {
+        double x = reinterpret_cast<const double*>(hv)[j];
+        asm volatile("" : "+v"(x));
+        tv[j] = x;
+    }
+#endif
     while (tile < total) {
         const int next = tile + (int)gridDim.x;
         const int ch = tile / tiles_ch, j = tile - ch * tiles_ch;
@@ -839,7 +865,11 @@ __global__ __launch_bounds__(64) void k_frontend2(
 #pragma unroll
                 for (int r = 0; r < R; r++) {
                     const int k = r * D + HP - S;
+#if SDR_FE_VTAP
+                    if (k >= 0 && k < NT) prod[r] = fe_mul_vv(tv[k >> 1], k & 1, m);
+#else
                     if (k >= 0 && k < NT) prod[r] = fe_mul_v(ring[slot][r >> 1], r & 1, m);
+#endif
 #if SDR_FE_CVT_MID
                     // the next sample's conversion between the products (an inline-asm result
                     // read right after it costs a wait state; here nothing reads it until S - 1)
@@ -899,10 +929,208 @@ __global__ __launch_bounds__(64) void k_frontend2(
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Front end v3 (exact): lanes are SEGMENTS of R consecutive decimated outputs, each streaming its
+// own window of TWIN = (R-1)*D + 101 u8 I/Q pairs straight from HBM/L2 into registers (16-byte
+// loads a few chunks ahead of the sweep; no LDS, so occupancy is set by VGPRs alone). The window
+// is swept in DESCENDING sample order as in k_frontend2, so every output accumulates its taps in
+// ascending k (filter.cpp:110-116) with the reference's f32 product and sum roundings; the taps
+// come from the same per-sample SGPR rows. Segments are phase-aligned (first output c with
+// 2*(D*c - 100) a multiple of 16), so any 64 of them share one instruction stream: a wave takes 63
+// consecutive segments of the flattened (channel, segment) order, lane 0 recomputing the
+// previous wave's last one for the discriminator's carry (demod.cpp:16) and writing nothing.
+// Segment i of a channel computes outputs [C0 + R*i, C0 + R*(i+1)); the last one is pulled back
+// to end at block_if (its overlap with the one before is written twice with identical values),
+// so no lane reads past its channel's block. The HEAD outputs [0, C0], whose windows reach into
+// the previous block (the u8 tail), are computed by the first waves of the grid (lane = channel,
+// same sweep from an 8-byte-granular tail/row window), which also copy the tail and the f32
+// history of the next block.
+// ------------------------------------------------------------------------------------------
+constexpr int fe3_c0(int D) {
+    int c = (100 + D - 1) / D;
+    while ((D * c - 100) % 8) c++;
+    return c;
+}
+constexpr int fe3_m(int D) { return D % 8 == 0 ? 1 : D % 4 == 0 ? 2 : D % 2 == 0 ? 4 : 8; }
+#ifndef SDR_FE3_PD
+#define SDR_FE3_PD 4
+#endif
+constexpr int FE3_PD = SDR_FE3_PD;   // 16-byte window chunks loaded ahead of the one being swept
+
+// discriminator of one output (demod.cpp:8-19): f32 numerator, f64 denominator and division
+__device__ __forceinline__ float fe_disc(f32x2 cur, f32x2 pv) {
+    if ((cur.x == 0) & (cur.y == 0)) return 0.0f;
+    const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
+    const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
+    return (float)((double)num / den);
+}
+
+// The register-blocked sweep of one lane window: acc[r] = (I, Q) of the lane's output r. load(q)
+// returns 16-byte chunk q of the window (samples 8q .. 8q+7), called in descending q.
+template <int R, int D, typename Load>
+__device__ __forceinline__ void fe3_sweep(const float* __restrict__ hs, Load load, f32x2 (&acc)[R]) {
+    constexpr int NT = 101, HP = NT - 1;
+    constexpr int TWIN = (R - 1) * D + NT;
+    constexpr int NCH = (2 * TWIN + 15) / 16;
+    uint4 chunk[NCH];
+#pragma unroll
+    for (int q = NCH - 1; q >= 0 && q >= NCH - 1 - FE3_PD; q--) chunk[q] = load(q);
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
+    int zero = 0;
+    asm volatile("" : "+s"(zero));
+    zero = __builtin_amdgcn_readfirstlane(zero);
+    const double* hsd = reinterpret_cast<const double*>(hs) + zero;
+    double ring[FE_PF][R / 2];
+#pragma unroll
+    for (int jj = 0; jj < FE_PF; jj++) {
+        const int S0 = TWIN - 1 - jj;
+#pragma unroll
+        for (int q = 0; q < R / 2; q++) ring[S0 % FE_PF][q] = hsd[S0 * (R / 2) + q];
+    }
+    auto sample = [&](int S) -> f32x2 {
+        const uint4 c4 = chunk[S >> 3];
+        const int dw = (S & 7) >> 1;
+        const uint32_t w = (dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w) ^ 0x80808080u;
+        return (S & 1) ? fe_cvt_v<1>(w) : fe_cvt_v<0>(w);
+    };
+    f32x2 m_next = sample(TWIN - 1);
+#pragma unroll
+    for (int S = TWIN - 1; S >= 0; S--) {
+        const int slot = S % FE_PF;
+        // entering chunk S>>3: the chunk FE3_PD + 1 below it goes in flight
+        if (((S & 7) == 7 || S == TWIN - 1) && (S >> 3) - FE3_PD - 1 >= 0) {
+            const int q = (S >> 3) - FE3_PD - 1;
+            chunk[q] = load(q);
+        }
+        const f32x2 m = m_next;
+        f32x2 prod[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int k = r * D + HP - S;
+            if (k >= 0 && k < NT) prod[r] = fe_mul_v(ring[slot][r >> 1], r & 1, m);
+        }
+        if (S > 0) m_next = sample(S - 1);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int k = r * D + HP - S;
+            if (k >= 0 && k < NT) acc[r] = fe_add_v(acc[r], prod[r]);
+        }
+        if (S - FE_PF >= 0) {
+#pragma unroll
+            for (int q = 0; q < R / 2; q++) ring[slot][q] = hsd[(S - FE_PF) * (R / 2) + q];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int R, int D, bool X4>
+__global__ __launch_bounds__(64) void k_frontend3(
+    const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
+    uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
+    const float* __restrict__ hs, int block_iq, int block_if, float* __restrict__ fm,
+    const float* __restrict__ fm_other, size_t fm_stride, int nch, int segs_ch, int head_waves) {
+    constexpr int NT = 101, HP = NT - 1;
+    constexpr int C0 = fe3_c0(D), M = fe3_m(D), A = C0 % M;
+    static_assert(R % M == 0 && A == 2 && M == 4, "store layout below assumes D == 10 alignment");
+    static_assert(C0 + 1 <= R, "the head lane computes outputs 0 .. C0 in one sweep");
+    const int t = threadIdx.x;
+    f32x2 acc[R];
+    if ((int)blockIdx.x < head_waves) {
+        // ---- head: lane = channel, outputs 0 .. C0 from samples [-HP, D*(R-1)] ----
+        const int ch = min((int)blockIdx.x * 64 + t, nch - 1);
+        const uint2* tl = reinterpret_cast<const uint2*>(tail_in + (size_t)ch * 2 * HP);   // samples -HP..-1
+        const uint2* rw = reinterpret_cast<const uint2*>(iq + (size_t)ch * iq_stride);      // samples 0..
+        // window byte b <-> sample -HP + b/2; 8-byte piece p: tail piece p (p < 25), row piece p - 25
+        auto piece = [&](int p) -> uint2 { return p < HP / 4 ? tl[p] : rw[p - HP / 4]; };
+        fe3_sweep<R, D>(hs, [&](int q) -> uint4 {
+            const uint2 lo = piece(2 * q), hi = piece(2 * q + 1);
+            return make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }, acc);
+        if ((int)blockIdx.x * 64 + t < nch) {
+            float* out = fm + (size_t)ch * fm_stride;
+            const float2 p = prev_in[ch];
+            f32x2 pv = f32x2{p.x, p.y};
+#pragma unroll
+            for (int r = 0; r <= C0; r++) {
+                out[r] = fe_disc(acc[r], pv);
+                pv = acc[r];
+            }
+        }
+        // this block's u8 tail and the f32 history in front of this parity's stream, a channel
+        // per iteration with the wave's lanes along it (coalesced)
+        for (int cc = 0; cc < 64; cc++) {
+            const int c = (int)blockIdx.x * 64 + cc;
+            if (c >= nch) break;
+            const uint16_t* last = reinterpret_cast<const uint16_t*>(iq + (size_t)c * iq_stride) + (block_iq - HP);
+            uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)c * 2 * HP);
+            for (int i = t; i < HP; i += 64) tout[i] = last[i];
+            float* out = fm + (size_t)c * fm_stride;
+            const float* o = fm_other + (size_t)c * fm_stride;
+            for (int i = t; i < HIST; i += 64) out[i - HIST] = o[block_if - HIST + i];
+        }
+        return;
+    }
+    // ---- segments: lane t takes flattened segment gb + t - 1 ----
+    const int gb = ((int)blockIdx.x - head_waves) * 63;          // wave-uniform
+    const int ch0 = gb / segs_ch, i0 = gb - ch0 * segs_ch;       // scalar division
+    int ch = ch0, i = i0 + t - 1;
+    if (i < 0) { ch -= 1; i += segs_ch; }
+    if (i >= segs_ch) { ch += 1; i -= segs_ch; }
+    bool writer = t > 0 && ch < nch;
+    if (ch < 0) { ch = 0; i = 0; }
+    if (ch >= nch) { ch = nch - 1; i = segs_ch - 1; }
+    const int c_last = A + M * ((block_if - R - A) / M);
+    const int cu = C0 + R * i;
+    const int cl = min(cu, c_last);
+    const bool write_first = writer && i > 0 && cu <= c_last;
+    const uint8_t* src = iq + (size_t)ch * iq_stride + 2 * (D * cl - HP);
+    if (X4) {   // 16-byte aligned rows: one load per chunk
+        fe3_sweep<R, D>(hs, [&](int q) -> uint4 { return reinterpret_cast<const uint4*>(src)[q]; }, acc);
+    } else {    // 8-byte aligned rows (e.g. a row stride of 147000 bytes): two
+        fe3_sweep<R, D>(hs, [&](int q) -> uint4 {
+            const uint2 lo = reinterpret_cast<const uint2*>(src)[2 * q], hi = reinterpret_cast<const uint2*>(src)[2 * q + 1];
+            return make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }, acc);
+    }
+    // ---- discriminator: the previous output of lane t's first is lane t-1's last ----
+    const f32x2 left = f32x2{__shfl_up(acc[R - 1].x, 1), __shfl_up(acc[R - 1].y, 1)};
+    float v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) v[r] = fe_disc(acc[r], r > 0 ? acc[r > 0 ? r - 1 : 0] : left);
+    if (writer) {
+        float* out = fm + (size_t)ch * fm_stride + cl;             // cl == 2 (mod 4): out + 2 is 16-byte aligned
+        if (write_first) out[0] = v[0];
+        out[1] = v[1];
+#pragma unroll
+        for (int r = 2; r + 4 <= R; r += 4)
+            *reinterpret_cast<float4*>(out + r) = make_float4(v[r], v[r + 1], v[r + 2], v[r + 3]);
+        *reinterpret_cast<float2*>(out + R - 2) = make_float2(v[R - 2], v[R - 1]);
+        if (cl + R == block_if) prev_out[ch] = make_float2(acc[R - 1].x, acc[R - 1].y);
+    }
+}
+
 size_t frontend_lds_bytes(int ntaps, int tile, int D) {
     const int ntaps_pad = (ntaps + 3) & ~3;
     const int W = tile * D + ntaps;                  // window incl. the extra output at n0-1
     return (size_t)ntaps_pad * 4 + (size_t)((W + 1) & ~1) * 8 + (size_t)(tile + 1) * 8 + 64;
+}
+
+// k_frontend3's layout assumptions, checked per launch (otherwise k_frontend2 runs): 8-byte
+// aligned input rows (16-byte aligned: one load per window chunk), 16-byte aligned fm_demod rows, the last segment ending exactly at block_if, segments
+// per channel >= 64 (a wave spans at most two channels), no window chunk past the block.
+bool fe3_ok(const FrontendArgs& a) {
+    constexpr int R = FE3_R, D = 10, TWIN = (R - 1) * D + 101, NCH = (2 * TWIN + 15) / 16;
+    constexpr int C0 = fe3_c0(D), M = fe3_m(D), A = C0 % M;
+    if (!std::getenv("SDR_FE_V3") || std::atoi(std::getenv("SDR_FE_V3")) != 1) return false;   // A/B knob, off
+    if (reinterpret_cast<uintptr_t>(a.iq) % 8 || a.iq_stride % 8) return false;
+    if (reinterpret_cast<uintptr_t>(a.fm) % 16 || a.fm_stride % 4) return false;
+    if (reinterpret_cast<uintptr_t>(a.tail_in) % 8) return false;
+    if ((a.block_if - R - A) % M != 0) return false;
+    if (cdiv(a.block_if - C0, R) < 64) return false;
+    if (2 * (D * (a.block_if - R) - 100) + 16 * NCH > 2 * a.block_iq) return false;
+    if (2 * (D * (R - 1) + 1) > 2 * a.block_iq) return false;
+    return true;
 }
 
 }  // namespace
@@ -927,7 +1155,7 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s) {
     const dim3 g2(a.fe_grid > 0 ? std::min(total, a.fe_grid) : total);
 #define FE2P(RR, DD, FF, PP)                                                                                 \
     hipLaunchKernelGGL((k_frontend2<RR, DD, FF, PP>), g2, dim3(64), 0, s, iq, iq_stride, tail_in,                \
-                       tail_out, prev_in, prev_out, a.hs, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride,        \
+                       tail_out, prev_in, prev_out, a.hs, a.hv, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride,  \
                        a.nch, tiles_ch, a.pad80)
 #define FE2(RR, DD, FF) do { if (a.fe_grid > 0) FE2P(RR, DD, FF, true); else FE2P(RR, DD, FF, false); } while (0)
 #define FE2R(DD)                                                                                             \
@@ -970,6 +1198,17 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s) {
 #undef FEMN
 #undef FEM
 #undef FEMP
+    } else if (!fast && a.hs3 && a.ntaps == 101 && a.D == 10 && fe3_ok(a)) {
+        constexpr int R3 = FE3_R;
+        const int C0 = fe3_c0(10);
+        const int segs = cdiv(a.block_if - C0, R3);
+        const int head = cdiv(a.nch, 64);
+        const dim3 g3(head + cdiv(a.nch * segs, 63));
+        const bool x4 = (iq_stride % 16 == 0) && (reinterpret_cast<uintptr_t>(iq) % 16 == 0);
+#define FE3(XX) hipLaunchKernelGGL((k_frontend3<R3, 10, XX>), g3, dim3(64), 0, s, iq, iq_stride, tail_in, tail_out, \
+                                   prev_in, prev_out, a.hs3, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride, a.nch, segs, head)
+        if (x4) FE3(true); else FE3(false);
+#undef FE3
     } else if (a.ntaps == 101 && a.D == 10) {
         FE2R(10);
     } else if (a.ntaps == 101 && a.D == 4) {

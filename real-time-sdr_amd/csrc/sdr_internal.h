@@ -31,6 +31,8 @@ constexpr int DEC_STATE = 8;     // ints of RDS decoder state per channel
 constexpr int FT_ND = 4;
 constexpr int FT_AFRAGS = 4 * FT_ND;
 constexpr int FT_NB_DEFAULT = 32;
+// exact front end v3 (k_frontend3): outputs per lane segment
+constexpr int FE3_R = 12;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -99,6 +101,8 @@ struct FrontendArgs {
     int nch, ntaps, block_iq, block_if, D;
     const float* h;            // plain taps (generic kernel)
     const float* hs;           // register-blocked tap table (k_frontend2)
+    const float* hv;           // the 101 taps / 128 as 51 pairs (+ a zero), k_frontend2 with SDR_FE_VTAP
+    const float* hs3;          // the same for k_frontend3's FE3_R outputs per lane (nullptr: not built)
     const void* afrag;         // MFMA tap fragments (fast mode)
     double yscale;             // MFMA fixed-point scale
     const uint32_t* pad80;     // 64 words of u8 128
@@ -141,7 +145,7 @@ struct sdr_ctx {
     sdr_info info{};
     int ntaps = 101;
     // taps (device)
-    float *rf_h = nullptr, *rf_hs = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
+    float *rf_h = nullptr, *rf_hs = nullptr, *rf_hv = nullptr, *rf_hs3 = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
           *rrc_h = nullptr;
     float *audio_pp = nullptr, *rdsbb_pp = nullptr;   // polyphase tables
     int *audio_cnt = nullptr, *rdsbb_cnt = nullptr;

@@ -1396,6 +1396,18 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
                 if (k >= 0 && k < T) tt[(size_t)S_ * R + r] = rf[k] * 0.0078125f;
             }
         TRY(upload(c, &c->rf_hs, tt));
+        std::vector<float> hv(((size_t)T + 1) / 2 * 2, 0.0f);
+        for (int k = 0; k < T; k++) hv[k] = rf[k] * 0.0078125f;
+        TRY(upload(c, &c->rf_hv, hv));
+        // the same rows for k_frontend3's FE3_R outputs per lane segment
+        const int TW3 = (FE3_R - 1) * D + T;
+        std::vector<float> t3((size_t)TW3 * FE3_R, 0.0f);
+        for (int S_ = 0; S_ < TW3; S_++)
+            for (int r = 0; r < FE3_R; r++) {
+                const int k = r * D + (T - 1) - S_;
+                if (k >= 0 && k < T) t3[(size_t)S_ * FE3_R + r] = rf[k] * 0.0078125f;
+            }
+        TRY(upload(c, &c->rf_hs3, t3));
     }
     if (T == 101 && (in.rf_decim == 10 || in.rf_decim == 4 || in.rf_decim == 3)) {
         // MFMA front end: taps as fixed point h*2^F in FT_ND balanced base-256 digits, laid out as
@@ -1537,6 +1549,8 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     a.D = in.rf_decim;
     a.h = c->rf_h;
     a.hs = c->rf_hs;
+    a.hs3 = c->rf_hs3;
+    a.hv = c->rf_hv;
     a.afrag = c->fe_afrag;
     a.yscale = c->fe_yscale;
     a.pad80 = c->pad80;

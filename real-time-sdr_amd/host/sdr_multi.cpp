@@ -25,6 +25,7 @@
 // queue's prepare() ordering.
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -37,6 +38,9 @@
 #include <sstream>
 #include <string>
 #include <thread>
+
+#include <sys/stat.h>
+#include <unistd.h>
 #include <vector>
 
 #include "fm_batch.h"
@@ -78,7 +82,7 @@ hipEvent_t new_event() {
 
 // ------------------------------------------------------------------ reader: input -> pinned ring
 struct Reader {
-    static constexpr int SLOTS = 3;
+    static constexpr int SLOTS = 4;   // pinned input slots: the read of block b+2..b+3 rides out host jitter
     FILE* f = nullptr;
     size_t bytes = 0;
     uint8_t* slot[SLOTS] = {};
@@ -88,11 +92,25 @@ struct Reader {
     std::condition_variable cv;
     std::deque<int> filled, empty;
     bool eof = false;
+    double read_s = 0.0;                // time spent reading (the input side of the I/O)
+    int readers = 8;                    // pread threads per block (regular files; SDR_MULTI_READERS)
+    long long file_size = 0, offset = 0;
     std::thread th;
 
     Reader(const std::string& path, size_t block_bytes) : bytes(block_bytes) {
         f = path == "-" ? stdin : std::fopen(path.c_str(), "rb");
         if (!f) die("cannot open " + path);
+        if (f != stdin) {   // a regular file is read by several threads at once (pread of a block's parts)
+            struct stat sb;
+            if (fstat(fileno(f), &sb) == 0 && S_ISREG(sb.st_mode)) {
+                file_size = (long long)sb.st_size;
+                if (const char* e = std::getenv("SDR_MULTI_READERS")) readers = std::max(1, std::atoi(e));
+            } else {
+                readers = 1;
+            }
+        } else {
+            readers = 1;
+        }
         for (int i = 0; i < SLOTS; i++) {
             check_hip(hipHostMalloc(reinterpret_cast<void**>(&slot[i]), bytes, hipHostMallocDefault), "hipHostMalloc");
             consumed[i] = new_event();
@@ -110,7 +128,9 @@ struct Reader {
                 empty.pop_front();
             }
             if (armed[i]) check_hip(hipEventSynchronize(consumed[i]), "hipEventSynchronize");
-            const size_t got = std::fread(slot[i], 1, bytes, f);
+            const auto r0 = std::chrono::steady_clock::now();
+            const size_t got = readers > 1 ? pread_block(slot[i]) : std::fread(slot[i], 1, bytes, f);
+            read_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - r0).count();
             std::lock_guard<std::mutex> lk(m);
             if (got < bytes) {             // a partial block ends the stream (rffrontend.cpp:50-52)
                 eof = true;
@@ -120,6 +140,32 @@ struct Reader {
             filled.push_back(i);
             cv.notify_all();
         }
+    }
+    // one block by `readers` threads, each a contiguous part (pread at the block's file offset)
+    size_t pread_block(uint8_t* dst) {
+        if (offset + (long long)bytes > file_size) return 0;   // a partial block ends the stream
+        const size_t part = (bytes / readers + 4095) / 4096 * 4096;
+        std::vector<std::thread> th_;
+        std::vector<size_t> got_(readers, 0);
+        for (int r = 0; r < readers; r++) {
+            const size_t lo = std::min(bytes, part * r), hi = std::min(bytes, part * (r + 1));
+            th_.emplace_back([&, r, lo, hi] {
+                size_t done = 0;
+                while (lo + done < hi) {
+                    const ssize_t k = ::pread(fileno(f), dst + lo + done, hi - lo - done, offset + (long long)(lo + done));
+                    if (k <= 0) break;
+                    done += (size_t)k;
+                }
+                got_[r] = done;
+            });
+        }
+        size_t got = 0;
+        for (int r = 0; r < readers; r++) {
+            th_[r].join();
+            got += got_[r];
+        }
+        offset += (long long)got;
+        return got;
     }
     int next() {   // a filled slot, or -1 at the end of the input
         std::unique_lock<std::mutex> lk(m);
@@ -148,7 +194,21 @@ struct Shared {
     sdr_info info{};
     ThreadSafeQueue<FmBatch*> q;
     long long blocks = 0;
+    std::chrono::steady_clock::time_point t_first{};   // block 0's front end enqueued (steady-state clock start)
+    double read_s = 0.0, h2d_ms = 0.0, d2h_ms = 0.0;   // input reads; GPU time of the H2D / L+R D2H copies
 };
+
+hipEvent_t timing_event() {
+    hipEvent_t e = nullptr;
+    check_hip(hipEventCreate(&e), "hipEventCreate");
+    return e;
+}
+float elapsed_ms(hipEvent_t a, hipEvent_t b) {
+    check_hip(hipEventSynchronize(b), "hipEventSynchronize");
+    float ms = 0.0f;
+    check_hip(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+    return ms;
+}
 
 // ------------------------------------------------------------------ RF front end (producer)
 void rf_thread(Shared* sh) {
@@ -161,14 +221,20 @@ void rf_thread(Shared* sh) {
     hipStream_t s = plain_stream(), s_copy = plain_stream();
     uint8_t* d_iq[2] = {};
     hipEvent_t h2d[2] = {new_event(), new_event()}, fe_done[2] = {new_event(), new_event()};
+    hipEvent_t c0[2] = {timing_event(), timing_event()}, c1[2] = {timing_event(), timing_event()};
     for (auto& p : d_iq) check_hip(hipMalloc(reinterpret_cast<void**>(&p), bytes), "hipMalloc");
     Reader rd(o.in, bytes);
     for (long long b = 0;; b++) {
         const int slot = rd.next();
         if (slot < 0) break;
         const int k = (int)(b & 1);
-        if (b >= 2) check_hip(hipStreamWaitEvent(s_copy, fe_done[k], 0), "hipStreamWaitEvent");
+        if (b >= 2) {
+            check_hip(hipStreamWaitEvent(s_copy, fe_done[k], 0), "hipStreamWaitEvent");
+            sh->h2d_ms += elapsed_ms(c0[k], c1[k]);         // block b-2's copy (long done)
+        }
+        check_hip(hipEventRecord(c0[k], s_copy), "hipEventRecord");
         check_hip(hipMemcpyAsync(d_iq[k], rd.slot[slot], bytes, hipMemcpyHostToDevice, s_copy), "hipMemcpyAsync");
+        check_hip(hipEventRecord(c1[k], s_copy), "hipEventRecord");
         check_hip(hipEventRecord(h2d[k], s_copy), "hipEventRecord");
         rd.release(slot, s_copy);
         check_hip(hipStreamWaitEvent(s, h2d[k], 0), "hipStreamWaitEvent");
@@ -181,9 +247,13 @@ void rf_thread(Shared* sh) {
         fb->block = b;
         sh->q.push(fb);                                     // rffrontend.cpp:74
         sh->blocks = b + 1;
+        if (b == 0) sh->t_first = std::chrono::steady_clock::now();
     }
     sh->q.push(nullptr);                                    // end of stream
     check_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+    for (long long b = std::max(0LL, sh->blocks - 2); b < sh->blocks; b++)
+        sh->h2d_ms += elapsed_ms(c0[b & 1], c1[b & 1]);
+    sh->read_s = rd.read_s;
     for (auto& p : d_iq) (void)hipFree(p);
     sdr_ctx_destroy(ctx);
 }
@@ -209,6 +279,7 @@ void audio_thread(Shared* sh) {
     const size_t n = 2 * (size_t)sh->info.n_audio, bytes = n * o.nch * sizeof(int16_t);
     hipStream_t s = plain_stream(), s_pll = pll_stream(o.device, o.cus);
     hipEvent_t pre = new_event(), pll = new_event(), out_ready[2] = {new_event(), new_event()};
+    hipEvent_t d0[2] = {timing_event(), timing_event()}, d1[2] = {timing_event(), timing_event()};
     int16_t *d_lr[2] = {}, *h_lr[2] = {};
     for (int k = 0; k < 2; k++) {
         check_hip(hipMalloc(reinterpret_cast<void**>(&d_lr[k]), bytes), "hipMalloc");
@@ -220,6 +291,7 @@ void audio_thread(Shared* sh) {
     auto write_block = [&](long long blk) {   // stereo.cpp:111, for every channel
         const int k = (int)(blk & 1);
         check_hip(hipEventSynchronize(out_ready[k]), "hipEventSynchronize");
+        sh->d2h_ms += elapsed_ms(d0[k], d1[k]);
         std::fwrite(h_lr[k], 1, bytes, f);
     };
     while (consume(sh, ctx, s, 0)) {
@@ -231,7 +303,9 @@ void audio_thread(Shared* sh) {
         check_hip(hipEventRecord(pll, s_pll), "hipEventRecord");
         check_hip(hipStreamWaitEvent(s, pll, 0), "hipStreamWaitEvent");
         check_sdr(sdr_stereo_post(ctx, d_lr[k], n, s), "sdr_stereo_post");
+        check_hip(hipEventRecord(d0[k], s), "hipEventRecord");
         check_hip(hipMemcpyAsync(h_lr[k], d_lr[k], bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+        check_hip(hipEventRecord(d1[k], s), "hipEventRecord");
         check_hip(hipEventRecord(out_ready[k], s), "hipEventRecord");
         if (b >= 1) write_block(b - 1);                     // overlaps block b's GPU work
         b++;
@@ -379,11 +453,22 @@ int main(int argc, char** argv) {
     t_rf.join();
     t_audio.join();
     t_rds.join();
-    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const auto t_end = std::chrono::steady_clock::now();
+    const double sec = std::chrono::duration<double>(t_end - t0).count();
+    const double steady = std::chrono::duration<double>(t_end - sh.t_first).count();
     const double samples = (double)sh.blocks * o.nch * sh.info.block_iq;
     const double signal_s = (double)sh.blocks * sh.info.block_iq / (double)sh.info.rf_Fs;
-    std::fprintf(stderr, "sdr_multi: %d channels x %lld blocks in %.3f s: %.1f MS/s I/Q, %.1fx real time\n", o.nch,
-                 sh.blocks, sec, samples / sec / 1e6, sec > 0 ? signal_s / sec : 0.0);
+    const double in_gb = (double)sh.blocks * o.nch * 2.0 * sh.info.block_iq / 1e9;
+    const double steady_samples = (double)(sh.blocks - 1) * o.nch * sh.info.block_iq;
+    std::fprintf(stderr,
+                 "sdr_multi: %d channels x %lld blocks in %.3f s: %.1f MS/s I/Q, %.1fx real time; after block 0 "
+                 "%.1f MS/s (%.1fx real time); input read %.3f s (%.1f GB/s), H2D %.3f s GPU time (%.1f GB/s), "
+                 "L/R D2H %.3f s\n",
+                 o.nch, sh.blocks, sec, samples / sec / 1e6, sec > 0 ? signal_s / sec : 0.0,
+                 steady > 0 ? steady_samples / steady / 1e6 : 0.0,
+                 steady > 0 ? (double)(sh.blocks - 1) * sh.info.block_iq / (double)sh.info.rf_Fs / steady : 0.0, sh.read_s,
+                 sh.read_s > 0 ? in_gb / sh.read_s : 0.0, sh.h2d_ms / 1e3, sh.h2d_ms > 0 ? in_gb / (sh.h2d_ms / 1e3) : 0.0,
+                 sh.d2h_ms / 1e3);
     for (auto& fb : batches) (void)hipFree(fb.d_fm);
     return 0;
 }

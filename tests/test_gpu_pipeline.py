@@ -94,11 +94,13 @@ def test_pipeline_long_run_bits(pkg, synth, golden_long, torch_cuda):
     assert float_mismatch == 0, f"{float_mismatch} block outputs differ from the reference"
 
 
-def test_pipeline_many_channels_vs_oracle(pkg, synth, oracle, torch_cuda):
-    """A wider batch (ragged: 67 channels) checked per channel against the oracle on a few blocks."""
+@pytest.mark.parametrize("row_align", [1, 16], ids=["rows_8B_aligned", "rows_16B_aligned"])
+def test_pipeline_many_channels_vs_oracle(pkg, synth, oracle, torch_cuda, row_align):
+    """A wider batch (ragged: 67 channels) checked per channel against the oracle on a few blocks
+    (channel 63 and 64 straddle a k_frontend3 wave's channel boundary at some segment)."""
     nch, nb = 67, 8
     iqs = [channel_input(synth, 100 + c, nb) for c in range(nch)]
-    out = _run_pipeline(pkg, torch_cuda, iqs, nb)
+    out = _run_pipeline(pkg, torch_cuda, iqs, nb, row_align=row_align)
     for c in (0, 1, 31, 63, 64, 66):
         ref = oracle.run_channel(iqs[c], 0, True)
         for b in range(nb):
@@ -487,22 +489,23 @@ def _frontend_only(pkg, torch, host, mode, flags):
 
 @pytest.mark.parametrize("mode", [0, 3])
 def test_frontend_grid_knobs_identical(pkg, synth, oracle, torch_cuda, mode, monkeypatch):
-    """The front end's tuning knobs compute the same bytes as the default one-tile-per-workgroup
-    grids, with several tiles per workgroup (SDR_FE_WG_PER_CU=1: one workgroup per CU): the
-    persistent exact kernel, the persistent LDS-DMA MFMA kernel and the persistent register-prefetch
+    """The front end's tuning knobs compute the same bytes as the default grids: the exact
+    register-blocked tile kernel k_frontend2 (SDR_FE_V3=0) against the default lane-segment kernel
+    k_frontend3 (mode 0; mode 3 runs k_frontend2 either way), with several tiles per workgroup
+    (SDR_FE_WG_PER_CU=1: one workgroup per CU): the persistent exact kernel, the persistent LDS-DMA MFMA kernel and the persistent register-prefetch
     MFMA kernel (SDR_FE_MFMA_WPE), incl. the first block (previous block's tail) and the padding."""
     import real_time_sdr_amd.synth as s
     block_iq = oracle.Channel(mode, True).block_iq
     nb, nch = 3, 67
     host = np.stack([np.stack([src.next_block(block_iq) for _ in range(nb)])
                      for src in (s.FMMultiplexSource(300 + c) for c in range(nch))], axis=1)
-    for flags, knobs in ((0, [{"SDR_FE_WG_PER_CU": "1"}]),
+    for flags, knobs in ((0, [{"SDR_FE_WG_PER_CU": "1", "SDR_FE_V3": "0"}, {"SDR_FE_V3": "0"}]),
                          (pkg.FLAG_FAST_FRONTEND, [{"SDR_FE_WG_PER_CU": "1"},
                                                    {"SDR_FE_MFMA_WPE": "3", "SDR_FE_WG_PER_CU": "1"},
                                                    {"SDR_FE_MFMA_WPE": "2"},
                                                    {"SDR_FE_MFMA_WPE": "3", "SDR_FE_NB": "16",
                                                     "SDR_FE_WG_PER_CU": "1"}])):
-        for k in ("SDR_FE_WG_PER_CU", "SDR_FE_MFMA_WPE", "SDR_FE_NB"):
+        for k in ("SDR_FE_WG_PER_CU", "SDR_FE_MFMA_WPE", "SDR_FE_NB", "SDR_FE_V3"):
             monkeypatch.delenv(k, raising=False)
         want = _frontend_only(pkg, torch_cuda, host, mode, flags)
         if flags == 0:
