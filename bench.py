@@ -181,6 +181,9 @@ class GpuStepper:
         self.s_fe, self.s_pll, self.s_post = s_fe, s_pll, s_post
         # SDR_BENCH_EDGES=0: the first and last block of a phase stay on their masked streams
         self.s_all = s_all if os.environ.get("SDR_BENCH_EDGES", "1") != "0" else None
+        # (not done: running the last block's stereo and RDS post stages side by side on a fifth
+        # CU-masked stream. A fifth dedicated hardware queue starves the front-end stream: the PLL then
+        # idles ~1 ms per 20 blocks waiting for input, 0.714 -> 0.78 ms/step, profiles/r03/drain2_ab.txt)
         self.phase = (0, -1)        # first and last block index of the current phase
         # SDR_BENCH_PLL=persistent (default): one PLL dispatch per phase (warm-up, timed) that waits
         # for each block's device flag (sdr_plls_launch/_signal/_wait); "dispatch": one sdr_plls
@@ -275,9 +278,10 @@ class GpuStepper:
         pipe.rds_post(self.clean, bits=True, stream=s_post)   # rds.cpp:122-167
         with torch.cuda.stream(s_post):
             bits.copy_(pipe.bits)
-            torch.index_select(lr, 0, self.vsel, out=self.cap_lr[b])
             torch.index_select(bits, 0, self.vsel, out=self.cap_bits[b])
             torch.index_select(pipe.nbits, 0, self.vsel, out=self.cap_nbits[b])
+        with torch.cuda.stream(s_post):
+            torch.index_select(lr, 0, self.vsel, out=self.cap_lr[b])
         self.post_done[b].record(s_post)
         if gather is not None:
             # final audio / bitstream gather to rank 0 over RCCL (xGMI), on its own non-blocking

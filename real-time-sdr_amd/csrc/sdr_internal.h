@@ -145,7 +145,7 @@ struct sdr_ctx {
     sdr_info info{};
     int ntaps = 101;
     // taps (device)
-    float *rf_h = nullptr, *rf_hs = nullptr, *rf_hv = nullptr, *rf_hs3 = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
+    float *rf_h = nullptr, *rf_hs = nullptr, *rf_hv = nullptr, *rf_hs3 = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *pilot_band_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
           *rrc_h = nullptr;
     float *audio_pp = nullptr, *rdsbb_pp = nullptr;   // polyphase tables
     int *audio_cnt = nullptr, *rdsbb_cnt = nullptr;

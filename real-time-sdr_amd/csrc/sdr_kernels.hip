@@ -137,6 +137,7 @@ constexpr int FRB_W = FRB_TILE + FRB_T - 1 + 3;   // staged samples (+3: whole 1
 // the other parity's row, copied in front by the first tile of each channel).
 struct FirRb {
     const float* h[3];
+    const float* h01;          // {h[0][k], h[1][k]} interleaved, padded to 104 pairs (k_fir_rb<3, *, true>)
     float* y[3];
     size_t y_stride[3];
     float* y0neg;
@@ -145,10 +146,27 @@ struct FirRb {
     const float* hist2_src;
 };
 
-template <int NT, bool SQUARE>
+#ifndef SDR_FRB_PK_ASM
+#define SDR_FRB_PK_ASM 0
+#endif
+// {h0, h1} * {v, v}: tap sets 0 and 1 of one sample in one packed multiply; the tap pair is an SGPR
+// pair, the sample the low (HI = 0) or high half of a VGPR pair, broadcast to both lanes by op_sel
+template <int HI>
+__device__ __forceinline__ f32x2 frb_pk_mul(double hpair, f32x2 wpair) {
+    f32x2 r;
+    if (HI) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "s"(hpair), "v"(wpair));
+    else asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(r) : "s"(hpair), "v"(wpair));
+    return r;
+}
+
+// PK (NT == 3): tap sets 0 and 1 (the stereo pilot and band BPFs) run as packed pairs -- one
+// v_pk_mul_f32 + one v_pk_add_f32 per sample and output for both, the same two roundings each as
+// filter.cpp:115 -- and set 2 (the RDS BPF) scalar: 4 VALU per sample and output instead of 6.
+template <int NT, bool SQUARE, bool PK = false>
 __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, size_t x_stride,
                                                 const float* __restrict__ hist, size_t hist_stride, int ny,
                                                 const FirRb f) {
+    static_assert(!PK || NT == 3, "packed pairs: sets 0 and 1 of a 3-set pass");
     constexpr int T = FRB_T, R = FRB_R;
     __shared__ __attribute__((aligned(16))) float sx[(FRB_W + 3) & ~3];
     const int ch = blockIdx.y, tid = threadIdx.x;
@@ -186,15 +204,72 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
         w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
     float a[NT][R];
+    constexpr int FRB_TC = 4;
+    constexpr int FRB_NC = (FRB_T + FRB_TC - 1) / FRB_TC;   // chunks (tap buffers are padded past 101)
+    typedef float f4v __attribute__((ext_vector_type(FRB_TC)));
+    if constexpr (PK) {
+        typedef float f8v __attribute__((ext_vector_type(2 * FRB_TC)));
+        f32x2 a01[R];
+        float a2[R];
+#pragma unroll
+        for (int j = 0; j < R; j++) { a01[j] = f32x2{0.0f, 0.0f}; a2[j] = 0.0f; }
+        f8v pb[2];                                       // {h0, h1} pairs of chunk c in pb[c & 1]
+        f4v sb[2];                                       // set 2's taps of chunk c
+        auto load8 = [&](f8v& d, int c) {
+            asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(d) : "s"(f.h01), "s"(c * FRB_TC * 8) : "memory");
+        };
+        auto load4 = [&](f4v& d, int c) {
+            asm volatile("s_load_dwordx4 %0, %1, %2" : "=s"(d) : "s"(f.h[2]), "s"(c * FRB_TC * 4) : "memory");
+        };
+        load8(pb[0], 0);
+        load4(sb[0], 0);
+        // the wait redefines the loaded registers, so no use of them is scheduled above it (a
+        // product hoisted above a plain waitcnt read the taps before they landed)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pb[0]), "+s"(sb[0]) :: "memory");
+#pragma unroll
+        for (int c = 0; c < FRB_NC; c++) {
+#pragma unroll
+            for (int kk = 0; kk < FRB_TC; kk++) {
+                const int k = c * FRB_TC + kk;
+                if (k < T) {
+                    const double hp = __builtin_bit_cast(double, f32x2{pb[c & 1][2 * kk], pb[c & 1][2 * kk + 1]});
+#pragma unroll
+                    for (int j = 0; j < R; j++) {
+                        const int i = j + T - 1 - k;
+#if SDR_FRB_PK_ASM
+                        const f32x2 wp = f32x2{w[i & ~1], w[i | 1]};
+                        const f32x2 pr = (i & 1) ? frb_pk_mul<1>(hp, wp) : frb_pk_mul<0>(hp, wp);
+#else
+                        // plain vector code: the compiler broadcasts the sample by op_sel (no copy)
+                        // and knows the packed result's latency (no inline-asm wait state)
+                        const f32x2 pr = __builtin_bit_cast(f32x2, hp) * f32x2{w[i], w[i]};
+#endif
+                        a01[j] = a01[j] + pr;                                  // filter.cpp:115
+                        a2[j] = a2[j] + sb[c & 1][kk] * w[i];
+                    }
+                }
+                if (kk == 0 && c + 1 < FRB_NC) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    load8(pb[(c + 1) & 1], c + 1);
+                    load4(sb[(c + 1) & 1], c + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            if (c + 1 < FRB_NC) {
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pb[(c + 1) & 1]), "+s"(sb[(c + 1) & 1]) :: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) { a[0][j] = a01[j].x; a[1][j] = a01[j].y; a[NT - 1][j] = a2[j]; }
+    } else {
 #pragma unroll
     for (int t = 0; t < NT; t++)
 #pragma unroll
         for (int j = 0; j < R; j++) a[t][j] = 0.0f;
     // taps: scalar loads issued by hand (the compiler would wait for every outstanding scalar load
     // at each tap's first use), one chunk of FRB_TC taps per tap set ahead
-    constexpr int FRB_TC = 4;
-    constexpr int FRB_NC = (FRB_T + FRB_TC - 1) / FRB_TC;   // chunks (tap buffers are padded past 101)
-    typedef float f4v __attribute__((ext_vector_type(FRB_TC)));
     f4v buf[2][NT];                                     // chunk c in buf[c & 1]
     // base address in an SGPR pair, byte offset in an SGPR (not one address pair per chunk)
     auto load = [&](f4v& d, const float* hp, int c) {
@@ -203,6 +278,8 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
 #pragma unroll
     for (int t = 0; t < NT; t++) load(buf[0][t], f.h[t], 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < NT; t++) asm volatile("" : "+s"(buf[0][t]));   // no tap use above the wait
 #pragma unroll
     for (int c = 0; c < FRB_NC; c++) {
 #pragma unroll
@@ -229,8 +306,11 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
         if (c + 1 < FRB_NC) {
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // chunk c + 1 landed
+#pragma unroll
+            for (int t = 0; t < NT; t++) asm volatile("" : "+s"(buf[(c + 1) & 1][t]));
             __builtin_amdgcn_sched_barrier(0);
         }
+    }
     }
     // every sum is complete here: otherwise the compiler sinks the second and third tap sets' products
     // past the first set's (divergent) stores and spills their taps from SGPRs
@@ -579,7 +659,7 @@ __device__ __forceinline__ void audio_mac(const float* __restrict__ h, const flo
 #pragma unroll
     for (int r = 0; r < AR; r++) acc[r] = 0.0f;
     load(buf[0], 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(buf[0]) :: "memory");   // no tap use above the wait
 #pragma unroll
     for (int c = 0; c < NC; c++) {
 #pragma unroll
@@ -597,7 +677,7 @@ __device__ __forceinline__ void audio_mac(const float* __restrict__ h, const flo
         }
         if (c + 1 < NC) {
             __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(buf[(c + 1) & 1]) :: "memory");
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -1445,6 +1525,12 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     }
     TRY(upload(c, &c->pilot_h, pilot));
     TRY(upload(c, &c->stereo_h, stereo));
+    {
+        // {pilot[k], band[k]} interleaved for the 3-filter pass's packed pairs, 104 pairs (chunks of 4)
+        std::vector<float> h01(2 * 104, 0.0f);
+        for (int k = 0; k < T && k < 104; k++) { h01[2 * k] = pilot[k]; h01[2 * k + 1] = stereo[k]; }
+        TRY(upload(c, &c->pilot_band_h, h01));
+    }
     TRY(upload(c, &c->rds_h, rds));
     TRY(upload(c, &c->rds_sq_h, rds_sq));
     TRY(upload(c, &c->rrc_h, rrc));
@@ -1615,6 +1701,16 @@ namespace {
 // launch k_fir_rb with NT tap sets (one block of every channel of length n)
 template <int NT, bool SQUARE>
 int fir_rb(const sdr_ctx* c, const float* x, size_t x_stride, int n, const FirRb& f, hipStream_t s) {
+    // the 3-set pass with its first two sets as packed pairs (SDR_FRB_PK=0: all scalar, A/B knob)
+    static const bool pk_env = !std::getenv("SDR_FRB_PK") || std::atoi(std::getenv("SDR_FRB_PK")) != 0;
+    if constexpr (NT == 3 && !SQUARE) {
+        if (f.h01 && pk_env) {
+            hipLaunchKernelGGL((k_fir_rb<3, false, true>), dim3(cdiv(n, FRB_TILE), c->nch), dim3(BLK), 0, s, x,
+                               x_stride, x, x_stride, n, f);
+            LAUNCH_CHECK();
+            return SDR_OK;
+        }
+    }
     hipLaunchKernelGGL((k_fir_rb<NT, SQUARE>), dim3(cdiv(n, FRB_TILE), c->nch), dim3(BLK), 0, s, x, x_stride, x,
                        x_stride, n, f);
     LAUNCH_CHECK();
@@ -1787,6 +1883,7 @@ int sdr_pre(sdr_ctx* c, void* stream) {
     // the third output goes into the extended rds_band stream, history included
     FirRb f = stereo_fir(c);
     f.h[2] = c->rds_h;
+    f.h01 = c->pilot_band_h;
     f.y[2] = c->rband + p * c->fm_par;
     f.y_stride[2] = c->fm_stride;
     f.hist2_src = c->rband + (p ^ 1) * c->fm_par;

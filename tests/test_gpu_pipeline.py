@@ -255,13 +255,15 @@ def test_fast_frontend_tolerance_and_rds_bits(pkg, synth, golden_long, oracle, t
                 assert _bitstr(out["bits"][b][j], int(out["nbits"][b][j])) == want["bits"], f"bits ch{c} block {b}"
 
 
-@pytest.mark.parametrize("fused_plls,cu_masked", [(False, False), (True, False), (True, True), ("persistent", True)],
-                         ids=["two_pll_streams", "sdr_plls", "sdr_plls_cu_masked", "persistent_cu_masked"])
-def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_plls, cu_masked):
+@pytest.mark.parametrize("fused_plls,cu_masked,pre3", [(False, False, False), (True, False, True), (True, True, False),
+                                                       ("persistent", True, True)],
+                         ids=["two_pll_streams", "sdr_plls_pre3", "sdr_plls_cu_masked", "persistent_cu_masked_pre3"])
+def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_plls, cu_masked, pre3):
     """bench.py's schedule: the stereo/RDS bodies split at the PLL (sdr_*_pre/_pll/_post, or both
     PLLs in one sdr_plls dispatch) on separate streams with the PLLs of block b+1 overlapping block
     b's post part -- identical audio, rds_clean and RDS bits to the one-stream sequential pipeline,
-    block by block."""
+    block by block. pre3: the pre-PLL FIRs as bench.py runs them (sdr_pre: the 3-filter pass with the
+    pilot and band filters as packed pairs) instead of sdr_stereo_pre + sdr_rds_pre."""
     torch = torch_cuda
     nch, nb = 40, 14
     iqs = [channel_input(synth, 300 + c, nb) for c in range(nch)]
@@ -298,8 +300,11 @@ def test_split_stages_on_streams_match_sequential(pkg, synth, torch_cuda, fused_
         pipe.mono(mono, stream=s_fe)
         with torch.cuda.stream(s_fe):
             got["mono"].append(mono.clone())
-        pipe.stereo_pre(stream=s_fe)
-        pipe.rds_pre(stream=s_fe)
+        if pre3:
+            pipe.pre(stream=s_fe)
+        else:
+            pipe.stereo_pre(stream=s_fe)
+            pipe.rds_pre(stream=s_fe)
         pre[b].record(s_fe)
         if fused_plls == "persistent":   # no events: device flags written / waited in stream order
             pipe.plls_signal(stream=s_fe)

@@ -89,7 +89,7 @@ def _run_schedule(torch, pkg, bench, iq, dev, schedule: str) -> dict:
     info = pipe.info
     created: list[int] = []
     try:
-        s_fe, s_pll, s_post = bench.cu_masked_streams(torch, pkg, dev, "64", created)
+        s_fe, s_pll, s_post, _ = bench.cu_masked_streams(torch, pkg, dev, "64", created)
     except (RuntimeError, AttributeError):
         if schedule == "persistent":
             pytest.skip("no CU-masked streams: the bench does not run the persistent PLL without them")

@@ -31,7 +31,7 @@ def main() -> None:
     n = pipe.info.block_if
     s = torch.cuda.Stream(dev)
     created: list[int] = []
-    _, s_pll, _ = bench.cu_masked_streams(torch, pkg, dev, "64", created)
+    _, s_pll, _, _ = bench.cu_masked_streams(torch, pkg, dev, "64", created)
     res = {"channels": nch, "chains": 2 * nch, "steps": n}
     lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device=dev)
     clean = torch.empty(nch, pipe.info.n_rds, dtype=torch.float32, device=dev)
