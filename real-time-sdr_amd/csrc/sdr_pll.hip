@@ -790,6 +790,12 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
 // wave and no waiting stream can hang.
 // ------------------------------------------------------------------------------------------
 constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrealtime
+#ifndef SDR_PLL_DIAG_RELAXED_DONE
+#define SDR_PLL_DIAG_RELAXED_DONE 0
+#endif
+#ifndef SDR_PLL_DIAG_NO_ACQUIRE
+#define SDR_PLL_DIAG_NO_ACQUIRE 0   // timing-only diagnosis: the cost of the per-block acquire
+#endif
 
 template <bool VEC, bool SPLIT>
 __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
@@ -820,10 +826,12 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
                     break;
                 }
             }
-            if (sys_acquire)
+            if (SDR_PLL_DIAG_NO_ACQUIRE) {
+            } else if (sys_acquire) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            else
+            } else {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
             if (dead && threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         unsigned long long c0 = 0, r0 = 0;   // this wave's shader-clock and 100 MHz stamps of the block
@@ -861,8 +869,13 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
                 __hip_atomic_fetch_add(t_cyc + 2 * j + 1, r1 - r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             // block sequence pre_first + j done by this wave: its own slot of the ring
+#if SDR_PLL_DIAG_RELAXED_DONE   // timing-only diagnosis (wrong memory ordering): the cost of the release
+            __hip_atomic_fetch_add(done_ring + (pre_first + (uint32_t)j) % PLL_DONE_RING, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#else
             __hip_atomic_fetch_add(done_ring + (pre_first + (uint32_t)j) % PLL_DONE_RING, 1u, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
+#endif
         }
     }
 }
