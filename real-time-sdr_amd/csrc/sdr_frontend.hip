@@ -774,12 +774,16 @@ __global__ __launch_bounds__(64) void k_frontend2(
     fetch(tile);
 #if SDR_FE_VTAP
     double tv[(NT + 1) / 2];          // tv[j] = {h[2j], h[2j+1]} / 128, uniform, held in VGPRs
+    auto load_taps = [&]() {
 #pragma unroll
-    for (int j = 0; j < (NT + 1) / 2; j++) {
-        double x = reinterpret_cast<const double*>(hv)[j];
-        asm volatile("" : "+v"(x));
-        tv[j] = x;
-    }
+        for (int j = 0; j < (NT + 1) / 2; j++) {
+            double x = reinterpret_cast<const double*>(hv)[j];
+            asm volatile("" : "+v"(x));
+            tv[j] = x;
+        }
+    };
+    // VTAP 1: before the window staging (tap and window registers overlap); 2: after it
+    if (SDR_FE_VTAP == 1) load_taps();
 #endif
     while (tile < total) {
         const int next = tile + (int)gridDim.x;
@@ -808,6 +812,9 @@ __global__ __launch_bounds__(64) void k_frontend2(
             }
         }
         __syncthreads();
+#if SDR_FE_VTAP
+        if (SDR_FE_VTAP == 2) load_taps();
+#endif
         if (PF && next < total) fetch(next);          // in flight during the FIR
         // ---- FIR: R outputs per thread, samples in descending order ----
         uint4 chunk[TCH];
