@@ -81,7 +81,7 @@ def launch_ranks(args, argv: list[str]) -> int:
 
 
 # ------------------------------------------------------------------------------ GPU stepper
-def cu_masked_streams(torch, pkg, dev, spec: str, created: list):
+def cu_masked_streams(torch, pkg, dev, spec: str, created: list, all_cus: bool = True):
     """(fe, pll, post, all) streams through the C ABI (sdr_stream_create_cu_range): the PLL stream
     on CUs [0, n), front end and post on the rest, and one stream over every CU for the pipeline's
     fill and drain (the first block's pre-PLL work and the last block's post-PLL work, when the PLL
@@ -96,13 +96,16 @@ def cu_masked_streams(torch, pkg, dev, spec: str, created: list):
     L.sdr_stream_create_cu_range.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int]
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     out = []
-    for lo, hi, exclude in ((0, n, 1), (0, n, 0), (0, n, 1), (0, ncu, 0)):
+    ranges = ((0, n, 1), (0, n, 0), (0, n, 1)) + (((0, ncu, 0),) if all_cus else ())
+    for lo, hi, exclude in ranges:
         h = C.c_void_p()
         rc = L.sdr_stream_create_cu_range(C.byref(h), dev.index, lo, hi, exclude)
         if rc != 0:
             raise RuntimeError(f"sdr_stream_create_cu_range: {rc} {L.sdr_last_error()}")
         created.append(h.value)
         out.append(torch.cuda.ExternalStream(h.value, device=dev))
+    if not all_cus:
+        out.append(None)
     return tuple(out)
 
 
@@ -172,7 +175,12 @@ class GpuStepper:
         cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64")
         if cu_spec not in ("", "0"):
             try:
-                s_fe, s_pll, s_post, s_all = cu_masked_streams(torch, pkg, dev, cu_spec, self.created)
+                # the all-CU fill/drain stream is a fourth dedicated hardware queue: at N > 1 RCCL's
+                # streams join the pool queues, so ranks keep three masked streams (a fifth queue
+                # starved the front end at N = 1)
+                world = int(os.environ.get("WORLD_SIZE", "1"))
+                s_fe, s_pll, s_post, s_all = cu_masked_streams(torch, pkg, dev, cu_spec, self.created,
+                                                               all_cus=world == 1)
             except (RuntimeError, ValueError, AttributeError) as exc:   # plain streams, reported
                 print(f"bench: CU-masked streams unavailable ({exc}); unmasked streams", file=sys.stderr)
                 destroy_masked_streams(torch, pkg, dev, self.created)
