@@ -403,11 +403,13 @@ class GpuStepper:
         f = getattr(self.pkg.lib(), "sdr_diag_pll_counts", None)
         if f is None:
             return None
-        c = (C.c_ulonglong * 4)()
+        c = (C.c_ulonglong * 10)()
         if f(c, 0) != 0 or c[0] == 0:
             return None
         return {"lane_chunks": c[0], "lane_fail_frac": c[1] / c[0], "wave_chunks": c[2],
-                "wave_redo_frac": c[3] / max(c[2], 1)}
+                "wave_redo_frac": c[3] / max(c[2], 1),
+                "lane_fail_by_reason": {"e_range": c[4], "e_bracket": c[5], "cos_sin_tie": c[6], "state": c[7]},
+                "lane_fail_by_job": {"stereo_19k": c[8], "rds_114k": c[9]}}
 
     def isolated_frontend(self) -> dict:
         """Outside the timed region: the front-end kernel of both numerics modes alone on the GPU
@@ -625,7 +627,7 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
                 res["roofline"]["copy_GBps"] = iso["hbm_copy"]["achieved"]
                 res["roofline"]["frac_of_copy"] = round(res["roofline"]["achieved"] / iso["hbm_copy"]["achieved"], 4)
                 res["roofline_fast"] = iso.get("fast")
-            res["cpu_baseline"] = (None if args.no_cpu_baseline else cpu_baseline_leg(args, None, timing=(world == 1)))
+            res["cpu_baseline"] = (None if args.no_cpu_baseline else cpu_baseline_leg(args, None, timing=(world == 1 and getattr(args, "cpu_timing", True))))
             if ver is not None:
                 res["cpu_baseline"]["verified"] = ver
             if gathered_check is not None:

@@ -110,7 +110,20 @@ constexpr double PLL_TAB_WT_MAX = 0x1.6p29;   // |w * trigOffset| bound of the t
 #endif
 #if SDR_PLL_COUNT
 // [lane-chunks, lane-chunks that failed their proof, wave-chunks, wave-chunks redone]
-__device__ unsigned long long g_pll_counts[4];
+// [4..7]: lane-chunks failing the e range, the e bracket, the cos/sin ties, the state range (a chunk
+// can fail several); [8], [9]: failed lane-chunks of job 0 (stereo 19 kHz) and job 1 (RDS 114 kHz)
+constexpr int PLL_NCOUNTS = 10;
+__device__ unsigned long long g_pll_counts[PLL_NCOUNTS];
+__device__ __forceinline__ void pll_count_reasons(bool emax_bad, bool split_bad, bool tie_bad, bool state_bad) {
+    const unsigned long long exec = __builtin_amdgcn_read_exec();
+    const unsigned long long m[4] = {__ballot(emax_bad) & exec, __ballot(split_bad) & exec, __ballot(tie_bad) & exec,
+                                     __ballot(state_bad) & exec};
+    const unsigned long long any = (m[0] | m[1] | m[2] | m[3]);
+    if ((int)__lane_id() == __ffsll((long long)exec) - 1) {
+        for (int k = 0; k < 4; k++) atomicAdd(&g_pll_counts[4 + k], (unsigned long long)__popcll(m[k]));
+        atomicAdd(&g_pll_counts[8 + (blockIdx.y & 1)], (unsigned long long)__popcll(any));
+    }
+}
 __device__ __forceinline__ void pll_count_chunk(bool ok) {
     const unsigned long long exec = __builtin_amdgcn_read_exec();
     const unsigned long long bad = __ballot(!ok) & exec;
@@ -676,6 +689,8 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
                             (TAB || (pf.tmax < 0x1p30f));
 #if SDR_PLL_COUNT
             pll_count_chunk(ok);
+            pll_count_reasons(!(pf.emaxf < PLL_EMAX_F), pf.split != 0u, !(pf.tie > pllm::TIE_MIN),
+                              !((__builtin_fabs(r.ip.y) < 0x1p28f) & (__builtin_fabs(r.ip.x) < 0x1p20f)));
 #endif
             // the partner's verdict, read with every lane of the pair active (under `ok && ...` the
             // exchange would sit in a branch, and a lane reading a disabled partner keeps its own value)
@@ -1111,12 +1126,13 @@ int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStrea
 }
 
 // Diagnosis builds only (-DSDR_PLL_COUNT=1): the PLL chunk counters [lane-chunks, failed lane-chunks,
-// wave-chunks, redone wave-chunks], optionally reset; -1 in product builds.
+// wave-chunks, redone wave-chunks, then per reason and per job (g_pll_counts)], 10 values,
+// optionally reset; -1 in product builds.
 int diag_pll_counts(unsigned long long* out, int reset) {
 #if SDR_PLL_COUNT
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pll_counts), sizeof(unsigned long long) * 4));
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pll_counts), sizeof(unsigned long long) * PLL_NCOUNTS));
     if (reset) {
-        const unsigned long long z[4] = {0, 0, 0, 0};
+        const unsigned long long z[PLL_NCOUNTS] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pll_counts), z, sizeof z));
     }
     return SDR_OK;

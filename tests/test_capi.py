@@ -40,7 +40,7 @@ def test_errors_are_status_codes(pkg):
 def test_diagnosis_counters_absent_in_product_build(pkg):
     """sdr_diag_pll_counts (not part of sdr_amd.h) only works in -DSDR_PLL_COUNT=1 diagnosis builds;
     the shipped library answers -1 without touching a GPU, and bench.py then reports no redo rate."""
-    out = (C.c_ulonglong * 4)()
+    out = (C.c_ulonglong * 10)()
     assert pkg.lib().sdr_diag_pll_counts(out, 0) == -1
 
 
