@@ -193,6 +193,7 @@ class GpuStepper:
         # CU-masked stream. A fifth dedicated hardware queue starves the front-end stream: the PLL then
         # idles ~1 ms per 20 blocks waiting for input, 0.714 -> 0.78 ms/step, profiles/r03/drain2_ab.txt)
         self.phase = (0, -1)        # first and last block index of the current phase
+        self.ev_fork, self.ev_join = torch.cuda.Event(), torch.cuda.Event()
         # SDR_BENCH_PLL=persistent (default): one PLL dispatch per phase (warm-up, timed) that waits
         # for each block's device flag (sdr_plls_launch/_signal/_wait); "dispatch": one sdr_plls
         # dispatch per block, ordered by events. The persistent kernel's waves spin until a later
@@ -282,14 +283,24 @@ class GpuStepper:
         if gather is not None and b >= 2:
             s_post.wait_event(self.gather_done[b - 2])        # lr/bits slot of block b-2 gathered
         lr, bits = self.lr[b % 2], self.bits[b % 2]
-        pipe.stereo_post(lr, stream=s_post)                   # stereo.cpp:83-107
+        # drain: the stereo post stage (its own buffers) beside the RDS one, on the post stream that
+        # is idle by then (no fifth hardware queue: DESIGN.md 5)
+        s_st = s_post
+        if edge_post:
+            s_st = self.s_post
+            self.ev_fork.record(s_post)
+            s_st.wait_event(self.ev_fork)
+        pipe.stereo_post(lr, stream=s_st)                     # stereo.cpp:83-107
         pipe.rds_post(self.clean, bits=True, stream=s_post)   # rds.cpp:122-167
         with torch.cuda.stream(s_post):
             bits.copy_(pipe.bits)
             torch.index_select(bits, 0, self.vsel, out=self.cap_bits[b])
             torch.index_select(pipe.nbits, 0, self.vsel, out=self.cap_nbits[b])
-        with torch.cuda.stream(s_post):
+        with torch.cuda.stream(s_st):
             torch.index_select(lr, 0, self.vsel, out=self.cap_lr[b])
+        if s_st is not s_post:
+            self.ev_join.record(s_st)
+            s_post.wait_event(self.ev_join)
         self.post_done[b].record(s_post)
         if gather is not None:
             # final audio / bitstream gather to rank 0 over RCCL (xGMI), on its own non-blocking
