@@ -167,6 +167,10 @@ int sdr_plls(sdr_ctx *ctx, void *stream);
  * Launching again while blocks of the previous launch were never signalled first lets that launch
  * time out and drain. Not with SDR_FLAG_PLL_LIBM. */
 int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
+/* Optional, ahead of sdr_plls_launch(nblocks) (e.g. before a timed region): the launch's
+ * bookkeeping -- allocation, the reset of its stamps and error word -- in `stream`'s order, so the
+ * launch itself only enqueues the kernel. Ignored by a launch with another nblocks. */
+int sdr_plls_prepare(sdr_ctx *ctx, int nblocks, void *stream);
 int sdr_plls_signal(sdr_ctx *ctx, void *stream);
 int sdr_plls_wait(sdr_ctx *ctx, void *stream);
 int sdr_plls_report(sdr_ctx *ctx, double *block_ms, int max_blocks, int *nblocks, void *stream);

@@ -90,6 +90,7 @@ def lib() -> C.CDLL:
         "sdr_rds_pll": ([vp, vp], i32),
         "sdr_plls": ([vp, vp], i32),
         "sdr_plls_launch": ([vp, i32, vp], i32),
+        "sdr_plls_prepare": ([vp, i32, vp], i32),
         "sdr_plls_signal": ([vp, vp], i32),
         "sdr_plls_wait": ([vp, vp], i32),
         "sdr_plls_report": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32), vp], i32),
@@ -326,6 +327,10 @@ class Pipeline:
     # persistent PLLs (include/sdr_amd.h): one dispatch for many blocks
     def plls_launch(self, nblocks: int, stream=None):
         check(lib().sdr_plls_launch(self._h, nblocks, _stream(stream)), "sdr_plls_launch")
+
+    def plls_prepare(self, nblocks: int, stream=None):
+        """The launch's bookkeeping ahead of plls_launch(nblocks) (allocation, stamp reset)."""
+        check(lib().sdr_plls_prepare(self._h, nblocks, _stream(stream)), "sdr_plls_prepare")
 
     def plls_signal(self, stream=None):
         check(lib().sdr_plls_signal(self._h, _stream(stream)), "sdr_plls_signal")

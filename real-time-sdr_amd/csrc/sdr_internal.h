@@ -191,6 +191,8 @@ struct sdr_ctx {
     unsigned long long *pers_t0 = nullptr, *pers_t1 = nullptr;
     unsigned long long* pers_cyc = nullptr;             // [block][2]: sums over waves of cycles, 100 MHz ticks
     int pers_tcap = 0, pers_last_n = 0;
+    int pers_prepared = 0;                              // sdr_plls_prepare's nblocks (0: none pending)
+    uint32_t pers_prepared_launch = 0;                  // pers_launched when it was prepared
     uint32_t pers_launched = 0, pers_signaled = 0, pers_waves = 0;
     uint32_t pers_base = 0;                             // sequence number of the last launch's first block
     uint32_t pers_waited = 0;                           // sequence numbers below this have been waited for

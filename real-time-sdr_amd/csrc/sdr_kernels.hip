@@ -1920,11 +1920,9 @@ int sdr_plls(sdr_ctx* c, void* stream) {
     return SDR_OK;
 }
 
-int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
-    if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_launch: bad arguments");
-    if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_launch: not with SDR_FLAG_PLL_LIBM");
-    HIP_TRY(hipSetDevice(c->device));
-    hipStream_t s = S(stream);
+// the bookkeeping of a persistent launch: recover an abandoned previous launch, allocate the words
+// and stamp arrays, reset this launch's stamps and error word (stream order on `stream`)
+static int plls_prepare(sdr_ctx* c, int nblocks, hipStream_t s) {
     if (c->pers_signaled != c->pers_launched) {
         // blocks of the previous launch were never signalled: its waves give up on them after the
         // bounded wait (PLL_WAIT_TICKS) and still count them done. Let it drain, then resynchronise
@@ -1961,6 +1959,30 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     HIP_TRY(hipMemsetAsync(c->pers_t1, 0, (size_t)nblocks * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(c->pers_cyc, 0, (size_t)nblocks * 2 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(c->pers_words + 1, 0, sizeof(uint32_t), s));   // err of this launch
+    c->pers_prepared = nblocks;
+    c->pers_prepared_launch = c->pers_launched;
+    return SDR_OK;
+}
+
+int sdr_plls_prepare(sdr_ctx* c, int nblocks, void* stream) {
+    if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_prepare: bad arguments");
+    if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_prepare: not with SDR_FLAG_PLL_LIBM");
+    HIP_TRY(hipSetDevice(c->device));
+    return plls_prepare(c, nblocks, S(stream));
+}
+
+int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
+    if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_launch: bad arguments");
+    if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_launch: not with SDR_FLAG_PLL_LIBM");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = S(stream);
+    // prepared ahead (sdr_plls_prepare, same nblocks, no launch since): only the launch is left
+    if (!(c->pers_prepared == nblocks && c->pers_prepared_launch == c->pers_launched &&
+          c->pers_signaled == c->pers_launched)) {
+        const int r = plls_prepare(c, nblocks, s);
+        if (r) return r;
+    }
+    c->pers_prepared = 0;
     const int n = c->info.block_if, nch = c->nch;
     PllJobs2 jobs{};
     const int first_parity = c->parity ^ 1;   // the parity the next sdr_frontend switches to: p[0]
