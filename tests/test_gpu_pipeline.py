@@ -399,7 +399,29 @@ def test_fast_frontend_all_outputs_tolerance(pkg, synth, golden_long, oracle, to
     assert not bad, f"{len(bad)} out of bounds: {bad[:12]}"
 
 
-def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda):
+@pytest.fixture
+def own_queue_stream(pkg, torch_cuda):
+    """Makes streams on CUs [0, 64) with their own hardware queue (sdr_stream_create_cu_range), as
+    the persistent launch requires (include/sdr_amd.h); destroyed after the test."""
+    import ctypes as C
+    L = pkg.lib()
+    L.sdr_stream_create_cu_range.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int]
+    L.sdr_stream_destroy.argtypes = [C.c_void_p]
+    made = []
+
+    def make():
+        h = C.c_void_p()
+        assert L.sdr_stream_create_cu_range(C.byref(h), torch_cuda.cuda.current_device(), 0, 64, 0) == 0
+        made.append(h.value)
+        return torch_cuda.cuda.ExternalStream(h.value)
+
+    yield make
+    torch_cuda.cuda.synchronize()
+    for h in made:
+        L.sdr_stream_destroy(C.c_void_p(h))
+
+
+def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda, own_queue_stream):
     """A persistent launch whose last block is never signalled ends by itself (bounded wait, 5 s),
     releases its done counter and reports the error; blocks before it are computed normally."""
     torch = torch_cuda
@@ -408,39 +430,42 @@ def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda):
     d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
     ref = _run_pipeline(pkg, torch, iqs, nb)
     pipe = pkg.Pipeline(nch)
-    s_pll, s_post = torch.cuda.Stream(), torch.cuda.Stream()
-    pipe.plls_launch(nb, stream=s_pll)
-    lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
-    for b in range(nb - 1):
-        pipe.frontend(d[b])
+    s_pll, s_post = own_queue_stream(), torch.cuda.Stream()   # the PLL stream owns its queue
+    # nothing on the legacy null stream while a launch is pending: the CU-masked PLL stream is a
+    # blocking stream, so null-stream work (and .cpu() copies on it) would wait for the launch
+    with torch.cuda.stream(torch.cuda.Stream()):
+        pipe.plls_launch(nb, stream=s_pll)
+        lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
+        for b in range(nb - 1):
+            pipe.frontend(d[b])
+            pipe.stereo_pre()
+            pipe.rds_pre()
+            pipe.plls_signal()
+            pipe.plls_wait(stream=s_post)
+            pipe.stereo_post(lr, stream=s_post)
+            pipe.rds_post(None, bits=False, stream=s_post)
+            s_post.synchronize()   # not torch.cuda.synchronize(): the persistent PLL is still running
+            assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
+        with pytest.raises(pkg.SdrError, match="timed out"):
+            pipe.plls_report(stream=s_pll)
+        # the context recovers: the abandoned block's PLL never ran (its state is still block 1's), a
+        # new launch resynchronises the sequence numbers and clears the error word, and block 2 then
+        # comes out as in the one-stream pipeline
+        pipe.plls_launch(1, stream=s_pll)
+        pipe.frontend(d[nb - 1])
         pipe.stereo_pre()
         pipe.rds_pre()
         pipe.plls_signal()
         pipe.plls_wait(stream=s_post)
         pipe.stereo_post(lr, stream=s_post)
         pipe.rds_post(None, bits=False, stream=s_post)
-        s_post.synchronize()   # not torch.cuda.synchronize(): the persistent PLL is still running
-        assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
-    with pytest.raises(pkg.SdrError, match="timed out"):
-        pipe.plls_report(stream=s_pll)
-    # the context recovers: the abandoned block's PLL never ran (its state is still block 1's), a
-    # new launch resynchronises the sequence numbers and clears the error word, and block 2 then
-    # comes out as in the one-stream pipeline
-    pipe.plls_launch(1, stream=s_pll)
-    pipe.frontend(d[nb - 1])
-    pipe.stereo_pre()
-    pipe.rds_pre()
-    pipe.plls_signal()
-    pipe.plls_wait(stream=s_post)
-    pipe.stereo_post(lr, stream=s_post)
-    pipe.rds_post(None, bits=False, stream=s_post)
-    s_post.synchronize()
-    assert np.array_equal(lr.cpu().numpy(), ref["stereo"][nb - 1]), "stereo after recovery"
-    assert len(pipe.plls_report(stream=s_pll)) == 1
+        s_post.synchronize()
+        assert np.array_equal(lr.cpu().numpy(), ref["stereo"][nb - 1]), "stereo after recovery"
+        assert len(pipe.plls_report(stream=s_pll)) == 1
     pipe.close()
 
 
-def test_persistent_plls_signal_checks_block_order(pkg, synth, torch_cuda):
+def test_persistent_plls_signal_checks_block_order(pkg, synth, torch_cuda, own_queue_stream):
     """A launch fixes each block's buffer parity from the block that follows it: signalling a block
     the launch does not cover next (here: the block that was already produced when the launch was
     made) is rejected; the blocks that do follow it run and match the one-stream pipeline."""
@@ -450,31 +475,36 @@ def test_persistent_plls_signal_checks_block_order(pkg, synth, torch_cuda):
     d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
     ref = _run_pipeline(pkg, torch, iqs, nb)
     pipe = pkg.Pipeline(nch)
-    s_pll, s_post = torch.cuda.Stream(), torch.cuda.Stream()
-    lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
-    pipe.frontend(d[0])
-    pipe.plls_launch(nb - 1, stream=s_pll)       # covers blocks 1 and 2
-    pipe.stereo_pre()
-    pipe.rds_pre()
-    with pytest.raises(pkg.SdrError, match="expects block 1"):
-        pipe.plls_signal()
-    pipe.stereo_pll()                            # block 0 the ordinary way
-    pipe.rds_pll()
-    pipe.stereo_post(lr)
-    pipe.rds_post(None, bits=False)
-    torch.cuda.current_stream().synchronize()
-    assert np.array_equal(lr.cpu().numpy(), ref["stereo"][0])
-    for b in range(1, nb):
-        pipe.frontend(d[b])
+    # the PLL stream owns its hardware queue (a CU-masked stream does, include/sdr_amd.h): on a
+    # pool stream the launch's waiting waves can sit in front of the signal on a shared queue
+    s_pll, s_post = own_queue_stream(), torch.cuda.Stream()
+    # nothing on the legacy null stream while a launch is pending: the CU-masked PLL stream is a
+    # blocking stream, so null-stream work (and .cpu() copies on it) would wait for the launch
+    with torch.cuda.stream(torch.cuda.Stream()):
+        lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
+        pipe.frontend(d[0])
+        pipe.plls_launch(nb - 1, stream=s_pll)       # covers blocks 1 and 2
         pipe.stereo_pre()
         pipe.rds_pre()
-        pipe.plls_signal()
-        pipe.plls_wait(stream=s_post)
-        pipe.stereo_post(lr, stream=s_post)
-        pipe.rds_post(None, bits=False, stream=s_post)
-        s_post.synchronize()
-        assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
-    assert len(pipe.plls_report(stream=s_pll)) == nb - 1
+        with pytest.raises(pkg.SdrError, match="expects block 1"):
+            pipe.plls_signal()
+        pipe.stereo_pll()                            # block 0 the ordinary way
+        pipe.rds_pll()
+        pipe.stereo_post(lr)
+        pipe.rds_post(None, bits=False)
+        torch.cuda.current_stream().synchronize()
+        assert np.array_equal(lr.cpu().numpy(), ref["stereo"][0])
+        for b in range(1, nb):
+            pipe.frontend(d[b])
+            pipe.stereo_pre()
+            pipe.rds_pre()
+            pipe.plls_signal()
+            pipe.plls_wait(stream=s_post)
+            pipe.stereo_post(lr, stream=s_post)
+            pipe.rds_post(None, bits=False, stream=s_post)
+            s_post.synchronize()
+            assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
+        assert len(pipe.plls_report(stream=s_pll)) == nb - 1
     pipe.close()
 
 
