@@ -525,8 +525,9 @@ def _frontend_only(pkg, torch, host, mode, flags):
 @pytest.mark.parametrize("mode", [0, 3])
 def test_frontend_grid_knobs_identical(pkg, synth, oracle, torch_cuda, mode, monkeypatch):
     """The front end's tuning knobs compute the same bytes as the default grids: the exact
-    register-blocked tile kernel k_frontend2 (SDR_FE_V3=0) against the default lane-segment kernel
-    k_frontend3 (mode 0; mode 3 runs k_frontend2 either way), with several tiles per workgroup
+    register-blocked tile kernel k_frontend2 against the lane-segment kernel k_frontend3
+    (SDR_FE_V3=1, a rejected A/B variant kept bit-exact; mode 0 only, mode 3 runs k_frontend2
+    either way), with several tiles per workgroup
     (SDR_FE_WG_PER_CU=1: one workgroup per CU): the persistent exact kernel, the persistent LDS-DMA MFMA kernel and the persistent register-prefetch
     MFMA kernel (SDR_FE_MFMA_WPE), incl. the first block (previous block's tail) and the padding."""
     import real_time_sdr_amd.synth as s
@@ -534,7 +535,7 @@ def test_frontend_grid_knobs_identical(pkg, synth, oracle, torch_cuda, mode, mon
     nb, nch = 3, 67
     host = np.stack([np.stack([src.next_block(block_iq) for _ in range(nb)])
                      for src in (s.FMMultiplexSource(300 + c) for c in range(nch))], axis=1)
-    for flags, knobs in ((0, [{"SDR_FE_WG_PER_CU": "1", "SDR_FE_V3": "0"}, {"SDR_FE_V3": "0"}]),
+    for flags, knobs in ((0, [{"SDR_FE_WG_PER_CU": "1"}, {"SDR_FE_V3": "1"}]),
                          (pkg.FLAG_FAST_FRONTEND, [{"SDR_FE_WG_PER_CU": "1"},
                                                    {"SDR_FE_MFMA_WPE": "3", "SDR_FE_WG_PER_CU": "1"},
                                                    {"SDR_FE_MFMA_WPE": "2"},
