@@ -202,10 +202,17 @@ class GpuStepper:
         # stream does (the runtime gives every stream with a CU mask a dedicated HSA queue instead
         # of sharing one from the pool), plain streams do not (GPU_MAX_HW_QUEUES = 4 pool queues are
         # shared by the torch streams, the gather stream and RCCL's): without masks -> dispatch.
+        # All of a persistent launch's waves must be resident at once: a lane pair per chain, 2 x nch
+        # chains, 64 lanes per wave, at most 2 waves per PLL CU (each holds the 59 KB trigArg table in
+        # LDS). Past that (4096 channels on 64 CUs) the blocks run as per-block dispatches.
         want = os.environ.get("SDR_BENCH_PLL", "persistent")
-        self.persist = want == "persistent" and bool(self.created)
-        self.pll_mode = ("persistent" if self.persist else "dispatch") + (
-            "" if want != "persistent" or self.persist else " (no CU-masked streams: persistent PLL not safe)")
+        pll_waves = -(-4 * nch // 64)
+        fits = bool(self.created) and pll_waves <= 2 * int(cu_spec or 0)
+        self.persist = want == "persistent" and fits
+        why = ("" if want != "persistent" or self.persist else
+               " (no CU-masked streams: persistent PLL not safe)" if not self.created else
+               f" ({pll_waves} PLL waves do not fit {cu_spec} CUs at once)")
+        self.pll_mode = ("persistent" if self.persist else "dispatch") + why
         self.s_gather = torch.cuda.Stream(dev)       # torch pool streams are non-blocking
         self.mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
         self.lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device=dev) for _ in range(2)]

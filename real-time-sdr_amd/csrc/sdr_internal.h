@@ -127,7 +127,7 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
 // may already finish the next block) and one shared count would release a block early.
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
-                     hipStream_t s);
+                     hipStream_t s, int max_cus);   // max_cus > 0: fail unless every wave fits max_cus CUs
 int launch_flag_store(uint32_t* flag, uint32_t v, hipStream_t s);
 int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStream_t s);
 int diag_pll_counts(unsigned long long* out, int reset);

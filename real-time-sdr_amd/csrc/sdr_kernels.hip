@@ -1995,7 +1995,7 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     }
     uint32_t waves = 0;
     const int r = launch_pll_multi(jobs, n, nch, nblocks, c->pers_words, c->pers_launched, c->pers_t0, c->pers_t1,
-                                   c->pers_cyc, &waves, s);
+                                   c->pers_cyc, &waves, s, c->cus);
     if (r) return r;
     c->pers_waves = waves;
     c->pers_base = c->pers_launched;

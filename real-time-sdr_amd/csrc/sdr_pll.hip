@@ -1086,7 +1086,7 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
 
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
-                     hipStream_t s) {
+                     hipStream_t s, int max_cus) {
     bool vec = true, split = !pll_nosplit_env();
     for (int k = 0; k < 2; k++)
         for (int q = 0; q < 2; q++) {
@@ -1101,6 +1101,15 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
     const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
     const dim3 g(cdiv(split ? 2 * nch : nch, 64), 2), b(64);
     *waves = g.x * g.y;
+    // every wave of a persistent launch must be resident at once (a wave that cannot start holds up
+    // the done count of every block, and the producer of later blocks waits for that): at most
+    // max_cus x what fits one CU (the LDS table, one wave per SIMD)
+    if (max_cus > 0) {
+        const int per_cu = std::min(4, tab_ok ? (int)(160 * 1024 / tab_bytes) : 4);
+        if ((int)*waves > max_cus * per_cu)
+            return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit %d CUs x %d resident waves: use sdr_plls",
+                        *waves, max_cus, per_cu);
+    }
     const char* acq = std::getenv("SDR_PLL_ACQUIRE");   // diagnosis: system-scope acquire
     const int sys_acq = (acq && std::strcmp(acq, "system") == 0) ? 1 : 0;
 #define KPM(V, SP)                                                                                       \
