@@ -202,16 +202,12 @@ class GpuStepper:
         # stream does (the runtime gives every stream with a CU mask a dedicated HSA queue instead
         # of sharing one from the pool), plain streams do not (GPU_MAX_HW_QUEUES = 4 pool queues are
         # shared by the torch streams, the gather stream and RCCL's): without masks -> dispatch.
-        # All of a persistent launch's waves must be resident at once: a lane pair per chain, 2 x nch
-        # chains, 64 lanes per wave, at most 2 waves per PLL CU (each holds the 59 KB trigArg table in
-        # LDS). Past that (4096 channels on 64 CUs) the blocks run as per-block dispatches.
+        # All of a persistent launch's waves must be resident on the PLL stream's CUs at once: the
+        # library checks that (and the stream's own hardware queue) and refuses the launch before any
+        # dispatch otherwise (4096 channels on 64 CUs); the blocks then run as per-block dispatches.
         want = os.environ.get("SDR_BENCH_PLL", "persistent")
-        pll_waves = -(-4 * nch // 64)
-        fits = bool(self.created) and pll_waves <= 2 * int(cu_spec or 0)
-        self.persist = want == "persistent" and fits
-        why = ("" if want != "persistent" or self.persist else
-               " (no CU-masked streams: persistent PLL not safe)" if not self.created else
-               f" ({pll_waves} PLL waves do not fit {cu_spec} CUs at once)")
+        self.persist = want == "persistent" and bool(self.created)
+        why = ("" if want != "persistent" or self.persist else " (no CU-masked streams: persistent PLL not safe)")
         self.pll_mode = ("persistent" if self.persist else "dispatch") + why
         self.s_gather = torch.cuda.Stream(dev)       # torch pool streams are non-blocking
         self.mono = torch.empty(nch, info.n_audio, dtype=torch.int16, device=dev)
@@ -247,11 +243,33 @@ class GpuStepper:
             self.torch.cuda.synchronize(self.dev)
 
     def begin_phase(self, nblocks: int) -> None:
-        """Before the warm-up and before the timed blocks: the persistent PLL dispatch of the phase."""
+        """Before the warm-up and before the timed blocks: the persistent PLL dispatch of the phase.
+        A launch the library refuses (before any dispatch: its waves would not all be resident on the
+        PLL stream's CUs) turns the bench to per-block dispatches, named in `pll.mode`."""
         if self.persist:
-            self.pipe.plls_launch(nblocks, stream=self.s_pll)
+            try:
+                self.pipe.plls_launch(nblocks, stream=self.s_pll)
+            except self.pkg.SdrError as exc:
+                self.persist = False
+                self.pll_mode = f"dispatch (persistent launch refused: {exc})"
         self.next_first = True
         self.phase_len = nblocks
+
+    @property
+    def launch_pending(self) -> bool:
+        """A phase's persistent PLL launch may be waiting for blocks (until the phase's synchronize)."""
+        return self.persist
+
+    def prime_gather(self, gather) -> None:
+        """N > 1, before the first phase: one untimed gather round (RCCL's lazy connection set-up runs
+        here, not beside a pending persistent launch) and the receiving rank's capture buffers, so
+        that inside a phase the per-step gather allocates nothing."""
+        torch = self.torch
+        with torch.cuda.stream(self.s_gather):
+            got = gather(lr=self.lr[0], bits=self.bits[0])
+            if got is not None:
+                self._alloc_capture(got)
+        torch.cuda.synchronize(self.dev)
 
     def step(self, b: int, gather=None) -> None:
         torch, pipe = self.torch, self.pipe
@@ -331,15 +349,20 @@ class GpuStepper:
         after the timed region (the gather buffers are reused every block-step)."""
         torch = self.torch
         world = len(got["lr"])
-        d = got["lr"][0].device
         if self.cap_g is None:
-            nv = self.vsel.numel()
-            self.vsel_g = self.vsel.to(d)
-            self.cap_g = {k: torch.empty((self.nblocks, world, nv) + tuple(got[k][0].shape[1:]), dtype=got[k][0].dtype,
-                                         device=d) for k in ("lr", "bits")}
+            raise RuntimeError("gather capture buffers not allocated (prime_gather before the first phase)")
         for k in ("lr", "bits"):
             for r in range(world):
                 torch.index_select(got[k][r], 0, self.vsel_g, out=self.cap_g[k][b, r])
+
+    def _alloc_capture(self, got: dict) -> None:
+        torch = self.torch
+        world = len(got["lr"])
+        d = got["lr"][0].device
+        nv = self.vsel.numel()
+        self.vsel_g = self.vsel.to(d)
+        self.cap_g = {k: torch.empty((self.nblocks, world, nv) + tuple(got[k][0].shape[1:]), dtype=got[k][0].dtype,
+                                     device=d) for k in ("lr", "bits")}
 
     def gathered_digests(self) -> list | None:
         """Receiving rank: per source rank, the digest of its gathered rows (compared with the digest
@@ -393,8 +416,7 @@ class GpuStepper:
                                else "k_pll: one dispatch per block") +
                               ", stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial chains",
                     "bound": "serial recurrence: block_if dependent steps per chain, " +
-                             ("one lane per chain" if os.environ.get("SDR_PLL_SPLIT") == "0"
-                              else "a lane pair per chain (cos / sin lanes)") +
+                             "a lane pair per chain (cos / sin lanes)" +
                              " (per-wave issue and dependent latency, DESIGN.md 4a)",
                     "mode": self.pll_mode,
                     "avg_launch_ms": round(pll_ms, 4), "ns_per_step": round(pll_ms * 1e6 / info.block_if, 2),
@@ -545,6 +567,81 @@ def _pmc_traffic(nch: int, numerics: str):
 
 
 # ------------------------------------------------------------------------------ rank path
+_DIST_CALLS = ("barrier", "all_reduce", "reduce", "broadcast", "all_gather", "all_gather_into_tensor", "gather",
+               "scatter", "reduce_scatter", "reduce_scatter_tensor", "all_to_all", "all_to_all_single", "send",
+               "recv", "isend", "irecv", "gather_object", "all_gather_object", "broadcast_object_list",
+               "batch_isend_irecv", "monitored_barrier")
+
+
+class LaunchWindow:
+    """The span of one phase from its persistent PLL launch to the phase's final synchronize. The
+    PLL stream is CU-masked, hence blocking: anything that synchronises the device implicitly (a
+    collective's set-up, a hipMalloc / hipFree of the caching allocator) would wait for the pending
+    launch until its 5 s bound. Inside the window every torch.distributed call but the per-step
+    gather (wrapped by gather()) raises, and a device allocation or free made inside it fails the
+    run at exit (torch.cuda.memory_stats num_device_alloc / num_device_free)."""
+
+    def __init__(self, torch, dist, device, active: bool):
+        self.torch, self.dist, self.active = torch, dist, active
+        self.device = torch.device(device) if not isinstance(device, str) else torch.device(device)
+        self.allow = False
+        self.saved = {}
+        self.log: list[str] = []
+
+    def _alloc_counts(self):
+        if self.device.type != "cuda":
+            return None
+        st = self.torch.cuda.memory_stats(self.device)
+        return st.get("num_device_alloc", 0), st.get("num_device_free", 0)
+
+    def __enter__(self):
+        if not self.active:
+            return self
+        self.log.append("open")
+        if self.dist.is_available() and self.dist.is_initialized():
+            for name in _DIST_CALLS:
+                fn = getattr(self.dist, name, None)
+                if fn is None:
+                    continue
+                self.saved[name] = fn
+
+                def guarded(*a, _fn=fn, _name=name, **k):
+                    if not self.allow:
+                        raise RuntimeError(f"torch.distributed.{_name} inside a pending persistent PLL launch "
+                                           "(only the per-step gather may run there)")
+                    return _fn(*a, **k)
+                setattr(self.dist, name, guarded)
+        self.alloc0 = self._alloc_counts()
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if not self.active:
+            return False
+        for name, fn in self.saved.items():
+            setattr(self.dist, name, fn)
+        self.saved = {}
+        self.log.append("close")
+        a1 = self._alloc_counts()
+        if et is None and self.alloc0 is not None and a1 != self.alloc0:
+            raise RuntimeError(f"device memory allocated or freed inside a pending persistent PLL launch "
+                               f"(hipMalloc/hipFree counts {self.alloc0} -> {a1})")
+        return False
+
+    def gather(self, fn):
+        """The per-step gather, the one collective allowed inside the window."""
+        if fn is None:
+            return None
+
+        def g(**tensors):
+            self.allow = True
+            try:
+                self.log.append("gather")
+                return fn(**tensors)
+            finally:
+                self.allow = False
+        return g
+
+
 def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, backend: str = "nccl") -> dict | None:
     """One rank of the benchmark: its own channel shard, W warm-up + K timed block-steps bracketed
     by barrier + synchronize, max over ranks, gather of each block-step's audio and RDS bits to
@@ -569,24 +666,35 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
     if world > 1 and not args.no_gather:
         bg = BlockGather(torch, dist, world, st.outputs_spec(), gdev, dst=0)
     gather = bg.gather if bg is not None else None
+    pending = bool(getattr(st, "launch_pending", False))
+    win_dev = gdev if world == 1 or backend == "nccl" else "cpu"
     try:
-        if hasattr(st, "begin_phase") and args.warmup:
-            st.begin_phase(args.warmup)
-        for b in range(args.warmup):
-            st.step(b, gather)
+        # RCCL connects lazily at a communicator's first collective: one untimed gather round (and
+        # the receiving rank's capture buffers) before any phase's persistent launch is pending
+        if gather is not None and hasattr(st, "prime_gather"):
+            st.prime_gather(gather)
         st.synchronize()
+        if world > 1:
+            dist.barrier()
+        with LaunchWindow(torch, dist, win_dev, pending) as win:
+            if hasattr(st, "begin_phase") and args.warmup:
+                st.begin_phase(args.warmup)
+            for b in range(args.warmup):
+                st.step(b, win.gather(gather))
+            st.synchronize()
         if world > 1:
             dist.barrier()
         if hasattr(st, "prepare_phase"):
             st.prepare_phase(args.steps)
         st.synchronize()
         t0 = time.perf_counter()
-        if hasattr(st, "begin_phase"):
-            st.begin_phase(args.steps)
-        for b in range(args.warmup, nblocks):
-            st.step(b, gather)
-        t_enq = time.perf_counter() - t0          # host time to enqueue the K block-steps
-        st.synchronize()
+        with LaunchWindow(torch, dist, win_dev, pending) as win:
+            if hasattr(st, "begin_phase"):
+                st.begin_phase(args.steps)
+            for b in range(args.warmup, nblocks):
+                st.step(b, win.gather(gather))
+            t_enq = time.perf_counter() - t0          # host time to enqueue the K block-steps
+            st.synchronize()
         if world > 1:
             dist.barrier()
         st.synchronize()

@@ -33,6 +33,11 @@ extern "C" {
 #define SDR_MAX_SYMS 256     /* symbols per block, >= n_rds/symbol_Fs + 1 for every mode */
 #define SDR_MAX_BITS 256
 
+/* Outputs of a block whose persistent PLL wait timed out (sdr_plls_launch): the post stages write
+ * these instead of audio / bits computed from phases that were never produced. */
+#define SDR_PCM_POISON ((int16_t)-32768)  /* every L/R sample of the block */
+#define SDR_NBITS_POISONED (-2)           /* nbits[ch] of sdr_rds_bits; rds_clean rows are NaN */
+
 /* Context flags */
 #define SDR_FLAG_FAST_FRONTEND 0x1  /* FMA front end: fm_demod within 1e-6 rel., not bit-exact */
 #define SDR_FLAG_PLL_LIBM 0x2       /* PLL via per-step f64 libm calls (A/B reference; env SDR_PLL=libm) */
@@ -156,16 +161,22 @@ int sdr_plls(sdr_ctx *ctx, void *stream);
  * first of those blocks; then per block, after both _pre parts, sdr_plls_signal on the stream that
  * ran them (instead of sdr_plls) and sdr_plls_wait on the stream of the _post parts. The kernel
  * waits for each block's signal (a device flag written in stream order), runs both PLLs, and
- * releases the waiting stream; a wait longer than 5 s ends the launch without computing and is
- * reported by sdr_plls_report, which also returns each block's PLL time of the last launch (ms,
- * from the device clock: its last wave's end minus the later of its signal and the previous
- * block's end) and synchronises `stream`. While a launch still waits for blocks, nothing may
- * synchronise with the PLL stream implicitly: a CU-masked stream is a blocking stream, so work on
- * the legacy null stream would wait for it (until the 5 s bound). Each block must be waited for
- * (sdr_plls_wait) before the 16th block after it is signalled. The PLL stream must own its hardware
- * queue (a CU-masked stream does): a kernel queued behind the waiting launch would never run.
- * Launching again while blocks of the previous launch were never signalled first lets that launch
- * time out and drain. Not with SDR_FLAG_PLL_LIBM. */
+ * releases the waiting stream. The PLL stream must be one sdr_stream_create_cu_range made (it owns
+ * its hardware queue; on a pool stream a signal could queue behind the waiting launch), and every
+ * wave of the launch must fit that stream's CUs at once: otherwise the launch is refused with
+ * SDR_E_INVALID before anything is dispatched (use sdr_plls). A wait longer than 5 s (a block
+ * never signalled, or a post stream that waits for a block the PLL never finished) ends the launch
+ * without computing: from then on the post stages of that launch's blocks write SDR_PCM_POISON
+ * audio, NaN rds_clean rows and nbits = SDR_NBITS_POISONED (never audio from phases the PLL did
+ * not produce), sdr_plls_report returns SDR_E_HIP, and after that report the post calls of those
+ * blocks fail too; sdr_ctx_reset + a new launch recover. sdr_plls_report also returns each
+ * block's PLL time of the last launch (ms, from the device clock: its last wave's end minus the
+ * later of its signal and the previous block's end) and synchronises `stream`. While a launch still
+ * waits for blocks, nothing may synchronise with the PLL stream implicitly: a CU-masked stream is a
+ * blocking stream, so work on the legacy null stream would wait for it (until the 5 s bound). Each
+ * block must be waited for (sdr_plls_wait) before the 16th block after it is signalled. Launching
+ * again while blocks of the previous launch were never signalled first lets that launch time out
+ * and drain. Not with SDR_FLAG_PLL_LIBM. */
 int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
 /* Optional, ahead of sdr_plls_launch(nblocks) (e.g. before a timed region): the launch's
  * bookkeeping -- allocation, the reset of its stamps and error word -- in `stream`'s order, so the

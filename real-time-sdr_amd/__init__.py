@@ -26,6 +26,8 @@ LIB_PATH = pathlib.Path(os.environ["SDR_AMD_LIB"]) if os.environ.get("SDR_AMD_LI
 SDR_OK = 0
 SDR_MAX_SYMS = 256
 SDR_MAX_BITS = 256
+SDR_PCM_POISON = -32768      # audio of a block whose persistent PLL wait timed out (include/sdr_amd.h)
+SDR_NBITS_POISONED = -2      # nbits of such a block (its rds_clean rows are NaN)
 FLAG_FAST_FRONTEND = 0x1
 FLAG_PLL_LIBM = 0x2
 FLAG_KEEP_INTERMEDIATES = 0x4

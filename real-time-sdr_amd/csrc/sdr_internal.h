@@ -112,7 +112,6 @@ struct FrontendArgs {
 int frontend_launch(const FrontendArgs& a, hipStream_t s);
 
 // ---- sdr_pll.hip
-bool pll_libm_env();
 int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s);
 int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s, bool with_nco = true);
 // the context-free fmpll primitive: reciprocals, PLL, NCO
@@ -200,6 +199,11 @@ struct sdr_ctx {
     hipStream_t pers_stream = nullptr;                  // stream of the last launch
     long long pers_block = -1;                          // block of the last signal
     uint32_t pers_block_seq = 0;                        // its sequence number
+    hipEvent_t pers_ev = nullptr;                       // orders a prepare on another stream after the last launch
+    bool pers_failed = false;                           // sdr_plls_report saw a timeout of the current launch
+    // the error word the post stages of the current block check (their outputs are poisoned when a
+    // persistent wait timed out): only for blocks signalled through a persistent launch
+    const uint32_t* post_err() const { return (pers_words && pers_block == block) ? pers_words + 1 : nullptr; }
     std::vector<void*> allocs;
 
     float* fm_cur() const { return fm + parity * fm_par; }

@@ -144,6 +144,7 @@ struct FirRb {
     double* rx0;
     size_t rx_stride;
     const float* hist2_src;
+    const uint32_t* err;       // non-null: poison the outputs (NaN) when *err != 0 (a persistent PLL timeout)
 };
 
 #ifndef SDR_FRB_PK_ASM
@@ -318,6 +319,12 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
     for (int t = 0; t < NT; t++)
 #pragma unroll
         for (int j = 0; j < R; j++) asm volatile("" : "+v"(a[t][j]));
+    if (f.err && *f.err != 0u) {                                  // no valid input behind this block
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int j = 0; j < R; j++) a[t][j] = __builtin_nanf("");
+    }
 #pragma unroll
     for (int t = 0; t < NT; t++) {
         float* o = f.y[t] + (size_t)ch * f.y_stride[t] + nb;
@@ -765,6 +772,7 @@ struct StereoOut {
     int n, ny;
     int16_t* lr;
     size_t lr_stride;
+    const uint32_t* err;        // non-null: a persistent PLL launch produced the phases (its error word)
 };
 
 template <int D>
@@ -774,6 +782,17 @@ __global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
     __shared__ __attribute__((aligned(16))) float sb[(WIN + 3) / 4 * 4 + 4];
     const int ch = blockIdx.y, tid = threadIdx.x;
     const int o0 = blockIdx.x * ATILE;
+    if (a.err && *a.err != 0u) {
+        // a persistent PLL wait timed out: this block's phases were never computed (or not yet),
+        // so the consumer gets a marked block instead of audio (include/sdr_amd.h SDR_PCM_POISON)
+        const int ob = o0 + tid * AR;
+        uint32_t* o = reinterpret_cast<uint32_t*>(a.lr + (size_t)ch * a.lr_stride) + ob;
+        const uint32_t pp = (uint32_t)(uint16_t)SDR_PCM_POISON * 0x10001u;
+#pragma unroll
+        for (int r = 0; r < AR; r++)
+            if (ob + r < a.ny) o[r] = pp;
+        return;
+    }
     const int m0 = D * o0 - 100;
     const bool last_tile = o0 + ATILE >= a.ny;
     // the last tile also computes up to the block end: stereo_dc's tail is the next block's history
@@ -831,6 +850,15 @@ __global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
             o[r] = (uint32_t)l | ((uint32_t)rr << 16);
         }
     }
+}
+
+// the unfused stereo post stage's poison (SDR_FLAG_KEEP_INTERMEDIATES): rows [nch][n] of int16
+// overwritten with SDR_PCM_POISON when a persistent PLL wait timed out
+__global__ __launch_bounds__(BLK) void k_poison_i16(const uint32_t* __restrict__ err, int16_t* __restrict__ p,
+                                                    size_t stride, int n) {
+    if (*err == 0u) return;
+    const int i = blockIdx.x * BLK + threadIdx.x;
+    if (i < n) p[(size_t)blockIdx.y * stride + i] = SDR_PCM_POISON;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -998,7 +1026,7 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
                                                  int32_t* __restrict__ offset_out, int32_t* __restrict__ nsym_out,
                                                  uint8_t* __restrict__ sym_out, size_t sym_stride,
                                                  int32_t* __restrict__ nbits_out, uint8_t* __restrict__ bits_out,
-                                                 size_t bits_stride) {
+                                                 size_t bits_stride, const uint32_t* __restrict__ err) {
     // dynamic LDS: 64 cdr sums, then the channel's whole block (n floats), staged with every load in
     // flight (the cdr reads it 39-strided and the slicer sps-strided: from LDS, not global memory)
     extern __shared__ int sums_dyn[];
@@ -1010,6 +1038,14 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
     const int block_count = d[0];
     const float* xc = x + (size_t)ch * x_stride;
     const bool decode = (block_count > 5) && rds_on;
+    if (err && *err != 0u) {   // a persistent PLL wait timed out: no bits from this block
+        if (lane == 0) {
+            if (offset_out) offset_out[ch] = -1;
+            if (nsym_out) nsym_out[ch] = 0;
+            if (nbits_out) nbits_out[ch] = SDR_NBITS_POISONED;
+        }
+        return;
+    }
     if (!decode) {
         if (lane == 0) {
             if (offset_out) offset_out[ch] = d[4];
@@ -1291,9 +1327,8 @@ PllJob rds_job(sdr_ctx* c) {      // rds.cpp:119: fmpll(gen_pilot, 114e3, if_Fs,
 namespace {
 // Scratch of the context-free PLL primitive (input reciprocals [nch][ts] f64 + phases [nch][ts]
 // f32): one buffer per (device, stream), reused in that stream's order and grown on demand, so
-// sdr_fmpll enqueues without synchronising. SDR_FMPLL_SCRATCH selects the older variants for the
-// diagnosis in DESIGN.md (tools/diag_fmpll_scratch.py): "sync" (hipMalloc, synchronise, hipFree),
-// "async" (two hipMallocAsync / hipFreeAsync pairs on the default pool).
+// sdr_fmpll enqueues without synchronising (the round-2 diagnosis of the pool-allocated variants
+// that this replaced: DESIGN.md 7, profiles/r02/diag_fmpll_scratch.txt).
 struct StreamScratch {
     hipStream_t s;
     int dev;
@@ -1340,16 +1375,26 @@ int release_stream_scratch(hipStream_t s) {
     return SDR_OK;
 }
 
-int fmpll_scratch_mode() {
-    static const int v = [] {
-        const char* e = std::getenv("SDR_FMPLL_SCRATCH");
-        if (e && std::strcmp(e, "sync") == 0) return 1;
-        if (e && std::strcmp(e, "async") == 0) return 2;
-        if (e && std::strcmp(e, "async_leak") == 0) return 3;      // hipMallocAsync, never freed
-        if (e && std::strcmp(e, "async_syncalloc") == 0) return 4; // hipMallocAsync + synchronise, then launch
-        return 0;
-    }();
-    return v;
+// Streams made by sdr_stream_create_cu_range, with their device and CU count. The persistent PLL
+// launch accepts only these: each has its own hardware queue (a pool stream can share one with the
+// stream that signals the blocks, which then never runs), and its CU count bounds how many of the
+// launch's waves can be resident at once.
+struct MaskedStream {
+    hipStream_t s;
+    int device, ncu;
+};
+std::mutex g_masked_mu;
+std::vector<MaskedStream> g_masked;
+
+bool masked_stream(hipStream_t s, int* device, int* ncu) {
+    std::lock_guard<std::mutex> lk(g_masked_mu);
+    for (const MaskedStream& m : g_masked)
+        if (m.s == s && s != nullptr) {
+            *device = m.device;
+            *ncu = m.ncu;
+            return true;
+        }
+    return false;
 }
 
 }  // namespace
@@ -1375,12 +1420,20 @@ int sdr_stream_create_cu_range(void** stream, int device, int first_cu, int n_cu
         return fail(SDR_E_INVALID, "sdr_stream_create_cu_range: CUs [%d, %d) outside [0, %d)",
                     first_cu, first_cu + n_cu, ncu);
     std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    int nset = 0;
     for (int cu = 0; cu < ncu; ++cu) {
         const bool in = cu >= first_cu && cu < first_cu + n_cu;
-        if (in != (exclude != 0)) mask[cu / 32] |= 1u << (cu % 32);
+        if (in != (exclude != 0)) {
+            mask[cu / 32] |= 1u << (cu % 32);
+            nset++;
+        }
     }
     hipStream_t s = nullptr;
     HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    {
+        std::lock_guard<std::mutex> lk(g_masked_mu);
+        g_masked.push_back(MaskedStream{s, device, nset});
+    }
     *stream = s;
     return SDR_OK;
 }
@@ -1389,6 +1442,14 @@ int sdr_stream_destroy(void* stream) {
     if (!stream) return fail(SDR_E_INVALID, "sdr_stream_destroy: stream is NULL");
     const int rc = release_stream_scratch((hipStream_t)stream);
     if (rc != SDR_OK) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_masked_mu);
+        for (size_t i = 0; i < g_masked.size(); i++)
+            if (g_masked[i].s == (hipStream_t)stream) {
+                g_masked.erase(g_masked.begin() + (long)i);
+                break;
+            }
+    }
     HIP_TRY(hipStreamDestroy((hipStream_t)stream));
     return SDR_OK;
 }
@@ -1595,6 +1656,7 @@ int sdr_ctx_destroy(sdr_ctx* c) {
     if (!c) return SDR_OK;
     (void)hipSetDevice(c->device);
     for (void* p : c->allocs) (void)hipFree(p);
+    if (c->pers_ev) (void)hipEventDestroy(c->pers_ev);
     delete c;
     return SDR_OK;
 }
@@ -1602,6 +1664,7 @@ int sdr_ctx_destroy(sdr_ctx* c) {
 int sdr_ctx_reset(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     HIP_TRY(hipSetDevice(c->device));
+    c->pers_failed = false;   // a timed-out launch's poisoned state is what the reset replaces
     return init_state(c, S(stream));
 }
 
@@ -1701,10 +1764,9 @@ namespace {
 // launch k_fir_rb with NT tap sets (one block of every channel of length n)
 template <int NT, bool SQUARE>
 int fir_rb(const sdr_ctx* c, const float* x, size_t x_stride, int n, const FirRb& f, hipStream_t s) {
-    // the 3-set pass with its first two sets as packed pairs (SDR_FRB_PK=0: all scalar, A/B knob)
-    static const bool pk_env = !std::getenv("SDR_FRB_PK") || std::atoi(std::getenv("SDR_FRB_PK")) != 0;
+    // the 3-set pass with its first two sets as packed pairs
     if constexpr (NT == 3 && !SQUARE) {
-        if (f.h01 && pk_env) {
+        if (f.h01) {
             hipLaunchKernelGGL((k_fir_rb<3, false, true>), dim3(cdiv(n, FRB_TILE), c->nch), dim3(BLK), 0, s, x,
                                x_stride, x, x_stride, n, f);
             LAUNCH_CHECK();
@@ -1755,10 +1817,20 @@ int sdr_stereo_pll(sdr_ctx* c, void* stream) {
     return SDR_OK;
 }
 
+// a persistent launch the host already knows timed out (sdr_plls_report): its blocks' post stages
+// fail (the device poisons their outputs anyway, for callers that have not asked yet)
+static int check_pers_failed(const sdr_ctx* c, const char* what) {
+    if (c->pers_failed && c->post_err())
+        return fail(SDR_E_HIP, "%s: the persistent PLL launch of this block timed out (outputs invalid): "
+                               "sdr_ctx_reset, then a new sdr_plls_launch", what);
+    return SDR_OK;
+}
+
 int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
     if (!c || !lr) return fail(SDR_E_INVALID, "null argument");
     if (c->st_pll_done != c->block || c->stereo_done == c->block)
         return fail(SDR_E_INVALID, "stereo_post: run sdr_stereo_pll on a new block first");
+    if (const int rf = check_pers_failed(c, "stereo_post")) return rf;
     const sdr_info& in = c->info;
     hipStream_t s = S(stream);
     const int n = in.block_if;
@@ -1787,6 +1859,7 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
         a.ny = in.n_audio;
         a.lr = lr;
         a.lr_stride = lr_stride;
+        a.err = c->post_err();
         const dim3 g(cdiv(in.n_audio, ATILE), c->nch);
         if (in.audio_decim == 5)
             hipLaunchKernelGGL(k_stereo_out<5>, g, dim3(AT), 0, s, a);
@@ -1819,6 +1892,11 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
                        c->fm_stride, c->fm_stride, c->audio_pp, c->audio_cnt, c->audio_L, in.audio_upsample,
                        in.audio_decim, in.n_audio, tile, -(HIST - 50), (void*)lr, lr_stride);
     LAUNCH_CHECK();
+    if (const uint32_t* err = c->post_err()) {
+        hipLaunchKernelGGL(k_poison_i16, dim3(cdiv(2 * in.n_audio, BLK), c->nch), dim3(BLK), 0, s, err, lr, lr_stride,
+                           2 * in.n_audio);
+        LAUNCH_CHECK();
+    }
     c->stereo_done = c->block;
     return SDR_OK;
 }
@@ -1923,6 +2001,7 @@ int sdr_plls(sdr_ctx* c, void* stream) {
 // the bookkeeping of a persistent launch: recover an abandoned previous launch, allocate the words
 // and stamp arrays, reset this launch's stamps and error word (stream order on `stream`)
 static int plls_prepare(sdr_ctx* c, int nblocks, hipStream_t s) {
+    int dev_unused = 0, ncu_unused = 0;
     if (c->pers_signaled != c->pers_launched) {
         // blocks of the previous launch were never signalled: its waves give up on them after the
         // bounded wait (PLL_WAIT_TICKS) and still count them done. Let it drain, then resynchronise
@@ -1930,6 +2009,14 @@ static int plls_prepare(sdr_ctx* c, int nblocks, hipStream_t s) {
         HIP_TRY(hipStreamSynchronize(c->pers_stream));
         c->pers_signaled = c->pers_waited = c->pers_launched;
         HIP_TRY(hipMemcpyAsync(c->pers_words, &c->pers_launched, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    } else if (c->pers_stream && c->pers_stream != s && c->pers_launched != 0 &&
+               masked_stream(c->pers_stream, &dev_unused, &ncu_unused)) {
+        // every block of the previous launch is signalled, but its waves may still be stamping its
+        // last blocks or setting its error word: the resets below wait for that launch in `s`'s order
+        // (a PLL stream destroyed since has completed its work: hipStreamDestroy waits for it)
+        if (!c->pers_ev) HIP_TRY(hipEventCreateWithFlags(&c->pers_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->pers_ev, c->pers_stream));
+        HIP_TRY(hipStreamWaitEvent(s, c->pers_ev, 0));
     }
     if (!c->pers_words) {
         void* w = nullptr;
@@ -1974,8 +2061,18 @@ int sdr_plls_prepare(sdr_ctx* c, int nblocks, void* stream) {
 int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_launch: bad arguments");
     if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_launch: not with SDR_FLAG_PLL_LIBM");
-    HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = S(stream);
+    // the launch's waves spin until later dispatches on other streams publish each block, so the
+    // PLL stream must own its hardware queue (pool streams share GPU_MAX_HW_QUEUES queues with the
+    // streams that signal) and every wave must fit the stream's CUs at once: refused before any
+    // dispatch otherwise (a waiting launch could never finish, and its blocks would time out)
+    int sdev = -1, scus = 0;
+    if (!masked_stream(s, &sdev, &scus))
+        return fail(SDR_E_INVALID, "plls_launch: the PLL stream was not made by sdr_stream_create_cu_range (a "
+                                   "persistent launch needs a stream with its own hardware queue; use sdr_plls)");
+    if (sdev != c->device)
+        return fail(SDR_E_INVALID, "plls_launch: the PLL stream is on device %d, the context on %d", sdev, c->device);
+    HIP_TRY(hipSetDevice(c->device));
     // prepared ahead (sdr_plls_prepare, same nblocks, no launch since): only the launch is left
     if (!(c->pers_prepared == nblocks && c->pers_prepared_launch == c->pers_launched &&
           c->pers_signaled == c->pers_launched)) {
@@ -1995,8 +2092,9 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     }
     uint32_t waves = 0;
     const int r = launch_pll_multi(jobs, n, nch, nblocks, c->pers_words, c->pers_launched, c->pers_t0, c->pers_t1,
-                                   c->pers_cyc, &waves, s, c->cus);
+                                   c->pers_cyc, &waves, s, scus);
     if (r) return r;
+    c->pers_failed = false;   // this launch's error word was cleared by its prepare
     c->pers_waves = waves;
     c->pers_base = c->pers_launched;
     c->pers_first_block = c->block + 1;       // the block the next sdr_frontend produces
@@ -2063,10 +2161,12 @@ int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, 
         block_ms[j] = (t1[j] >= from) ? (double)(t1[j] - from) * 1e-5 : -1.0;
     }
     if (nblocks) *nblocks = n;
-    if (words[1])
+    if (words[1]) {
+        c->pers_failed = true;
         return fail(SDR_E_HIP, "plls_report: a persistent PLL wait timed out (outputs invalid): err %u, flag %u, "
                     "signalled %u, launched %u, waves %u", words[1], words[0], c->pers_signaled, c->pers_launched,
                     c->pers_waves);
+    }
     return SDR_OK;
 }
 
@@ -2106,6 +2206,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (c->rds_pll_done != c->block || c->rds_dsp_done == c->block)
         return fail(SDR_E_INVALID, "rds_post: run sdr_rds_pll on a new block first");
+    if (const int rf = check_pers_failed(c, "rds_post")) return rf;
     const sdr_info& in = c->info;
     hipStream_t s = S(stream);
     const int n = in.block_if, T = c->ntaps, p = c->parity;
@@ -2163,6 +2264,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         f.h[0] = c->rrc_h;
         f.y[0] = dst;
         f.y_stride[0] = dst_stride;
+        f.err = c->post_err();                      // NaN rows after a persistent PLL timeout
         const int r = fir_rb<1, false>(c, rfilt, c->rf_stride, in.n_rds, f, s);
         if (r) return r;
     }
@@ -2188,11 +2290,12 @@ int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, s
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (c->rds_dsp_done != c->block || c->rds_bits_done == c->block)
         return fail(SDR_E_INVALID, "rds_bits: run sdr_rds_dsp on a new block first");
+    if (const int rf = check_pers_failed(c, "rds_bits")) return rf;
     const sdr_info& in = c->info;
     hipLaunchKernelGGL(k_rds_bits, dim3(c->nch), dim3(64), 64 * sizeof(int) + (size_t)in.n_rds * sizeof(float),
                        S(stream), c->rds_clean,
                        c->clean_stride, in.n_rds, in.symbol_Fs, c->rds_on, c->dec, offset, nsym, symbols,
-                       sym_stride, nbits, bits, bits_stride);
+                       sym_stride, nbits, bits, bits_stride, c->post_err());
     LAUNCH_CHECK();
     c->rds_bits_done = c->block;
     return SDR_OK;
@@ -2329,40 +2432,19 @@ int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, 
     const size_t ts = round_up((size_t)std::max(n, 1), 4);
     // scratch: input reciprocals (f64), phases and -in (f32), each [nch][ts]
     const size_t rx_bytes = ts * nch * sizeof(double), t_bytes = 2 * ts * nch * sizeof(float);
-    const int mode = fmpll_scratch_mode();
     hipStream_t s = S(stream);
-    if (mode >= 2) {
-        void *rxp = nullptr, *tp = nullptr;
-        HIP_TRY(hipMallocAsync(&rxp, rx_bytes, s));
-        HIP_TRY(hipMallocAsync(&tp, t_bytes, s));
-        if (mode == 4) HIP_TRY(hipStreamSynchronize(s));
-        const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, static_cast<float*>(tp), ts,
-                                 static_cast<double*>(rxp), static_cast<float*>(tp) + ts * nch, out, out_stride,
-                                 state, ncoScale, phaseAdjust, normBandwidth, s);
-        if (mode != 3) {
-            HIP_TRY(hipFreeAsync(rxp, s));
-            HIP_TRY(hipFreeAsync(tp, s));
-        }
-        return r;
-    }
+    // one scratch buffer per stream, reused in that stream's order (buffers from the
+    // stream-ordered pool, hipMallocAsync / hipFreeAsync per call, came back wrong)
     void* scratch = nullptr;
-    std::unique_lock<std::mutex> lk(g_scratch_mu, std::defer_lock);
-    if (mode == 1) {
-        HIP_TRY(hipMalloc(&scratch, rx_bytes + t_bytes));
-    } else {
-        lk.lock();   // held until the PLL kernels are enqueued
+    std::unique_lock<std::mutex> lk(g_scratch_mu);   // held until the PLL kernels are enqueued
+    {
         const int rc = stream_scratch(s, rx_bytes + t_bytes, &scratch);
         if (rc != SDR_OK) return rc;
     }
     double* rxbuf = static_cast<double*>(scratch);
     float* tbuf = reinterpret_cast<float*>(rxbuf + ts * nch);
-    const int r = launch_pll(false, in, in_stride, n, nch, freq, Fs, tbuf, ts, rxbuf, tbuf + ts * nch, out, out_stride,
-                             state, ncoScale, phaseAdjust, normBandwidth, s);
-    if (mode == 1) {
-        HIP_TRY(hipStreamSynchronize(s));
-        HIP_TRY(hipFree(scratch));
-    }
-    return r;
+    return launch_pll(false, in, in_stride, n, nch, freq, Fs, tbuf, ts, rxbuf, tbuf + ts * nch, out, out_stride,
+                      state, ncoScale, phaseAdjust, normBandwidth, s);
 }
 
 int sdr_cdr(int32_t* offset, const float* x, size_t x_stride, int nch, int n, int sps, void* stream) {

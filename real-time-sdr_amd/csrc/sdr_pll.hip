@@ -397,13 +397,7 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
                 for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
             }
             // refill (the last refills re-read the final chunk: harmless, keeps the loop branch-free)
-#if SDR_PLL_DIAG_L2
-            // diagnosis only (wrong results): every refill re-reads the first chunks (L2-resident),
-            // to measure what the HBM latency of the refills costs
-            load_chunk(xb[u], rb[u], u * C);
-#else
             load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
-#endif
 #if SDR_PLL_W01
             if (TAB) w01 = reinterpret_cast<const double2*>(wtab)[min(i0 + C, n - 2) >> 1];
 #endif
@@ -805,19 +799,13 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
 // wave and no waiting stream can hang.
 // ------------------------------------------------------------------------------------------
 constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrealtime
-#ifndef SDR_PLL_DIAG_RELAXED_DONE
-#define SDR_PLL_DIAG_RELAXED_DONE 0
-#endif
-#ifndef SDR_PLL_DIAG_NO_ACQUIRE
-#define SDR_PLL_DIAG_NO_ACQUIRE 0   // timing-only diagnosis: the cost of the per-block acquire
-#endif
 
 template <bool VEC, bool SPLIT>
 __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
                                                   const uint32_t* pre_flag, uint32_t pre_first,
                                                   uint32_t* done_ring, uint32_t* err,
                                                   unsigned long long* t_start, unsigned long long* t_end,
-                                                  unsigned long long* t_cyc, int sys_acquire) {
+                                                  unsigned long long* t_cyc) {
     extern __shared__ double wtab[];
     const int lg = blockIdx.x * blockDim.x + threadIdx.x;
     const int ch = SPLIT ? lg >> 1 : lg;
@@ -832,21 +820,14 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
             // poll with relaxed loads and acquire once: an acquire load at agent scope invalidates
             // the wave's caches (on a multi-XCD device its XCD's L2) on every poll, which slowed the
             // kernels running beside the waiting waves 2-3x
-            while ((int32_t)((sys_acquire ? __hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                          : __hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
-                             want) < 0) {
+            while ((int32_t)(__hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
                 __builtin_amdgcn_s_sleep(4);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
                     dead = true;
                     break;
                 }
             }
-            if (SDR_PLL_DIAG_NO_ACQUIRE) {
-            } else if (sys_acquire) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            } else {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             if (dead && threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         unsigned long long c0 = 0, r0 = 0;   // this wave's shader-clock and 100 MHz stamps of the block
@@ -884,13 +865,8 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
                 __hip_atomic_fetch_add(t_cyc + 2 * j + 1, r1 - r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             // block sequence pre_first + j done by this wave: its own slot of the ring
-#if SDR_PLL_DIAG_RELAXED_DONE   // timing-only diagnosis (wrong memory ordering): the cost of the release
-            __hip_atomic_fetch_add(done_ring + (pre_first + (uint32_t)j) % PLL_DONE_RING, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-#else
             __hip_atomic_fetch_add(done_ring + (pre_first + (uint32_t)j) % PLL_DONE_RING, 1u, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
-#endif
         }
     }
 }
@@ -1002,37 +978,18 @@ __global__ __launch_bounds__(BLK) void k_nco_out(const PllJobs jobs, int n) {
     if (i == n - 1) st[ch].lastCarrier = v;
     if (i == 0 && jb.prev_out) o[-1] = jb.prev_out[(size_t)ch * out_stride + n];
 }
-// PLL + NCO output: k_pll (fast, default) or k_pll_libm (SDR_FLAG_PLL_LIBM / env SDR_PLL=libm)
+// PLL + NCO output: k_pll (fast, default) or k_pll_libm (SDR_FLAG_PLL_LIBM)
 }  // namespace
 
-bool pll_libm_env() {
-    static const bool v = [] {
-        const char* e = std::getenv("SDR_PLL");
-        return e && std::strcmp(e, "libm") == 0;
-    }();
-    return v;
-}
-
-namespace {
-// SDR_PLL_SPLIT=0: one lane per channel even where the producer wrote -x (A/B of the lane pairs)
-bool pll_nosplit_env() {
-    static const bool v = [] {
-        const char* e = std::getenv("SDR_PLL_SPLIT");
-        return e && std::strcmp(e, "0") == 0;
-    }();
-    return v;
-}
-
-// SDR_PLL_TAB=0: per-lane trigArg offsets (A/B of the LDS table)
-bool pll_notab_env() {
-    static const bool v = [] {
-        const char* e = std::getenv("SDR_PLL_TAB");
-        return e && std::strcmp(e, "0") == 0;
-    }();
-    return v;
-}
-
-}  // namespace
+// compile-time A/B switches for variant builds (tools/build_variant.sh), never read at run time:
+// SDR_PLL_NOSPLIT=1 one lane per channel even where the producer wrote -x (the lane pairs off),
+// SDR_PLL_NOTAB=1 per-lane trigArg offsets (the LDS table off)
+#ifndef SDR_PLL_NOSPLIT
+#define SDR_PLL_NOSPLIT 0
+#endif
+#ifndef SDR_PLL_NOTAB
+#define SDR_PLL_NOTAB 0
+#endif
 
 int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
     if (n > 0) {
@@ -1043,7 +1000,7 @@ int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
 }
 
 int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s, bool with_nco) {
-    bool vec = true, split = !pll_nosplit_env();
+    bool vec = true, split = !SDR_PLL_NOSPLIT;
     for (int k = 0; k < njobs; k++) {
         const PllJob& j = jobs.j[k];
         vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
@@ -1055,9 +1012,9 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
     const dim3 g(cdiv(split ? 2 * nch : nch, 64), njobs), b(64);
     // LDS table of w * trigOffset (k_pll): n doubles, 16-byte rows
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
-    const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
+    const int tab_ok = (tab_bytes <= 64 * 1024 && !SDR_PLL_NOTAB) ? 1 : 0;
     const size_t lds = tab_ok ? tab_bytes : 0;
-    if (libm || pll_libm_env()) {
+    if (libm) {
         hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, jobs, n, nch);
     } else if (vec) {
         if (split) hipLaunchKernelGGL((k_pll<true, true>), g, b, lds, s, jobs, n, nch, tab_ok);
@@ -1087,7 +1044,7 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
                      hipStream_t s, int max_cus) {
-    bool vec = true, split = !pll_nosplit_env();
+    bool vec = true, split = !SDR_PLL_NOSPLIT;
     for (int k = 0; k < 2; k++)
         for (int q = 0; q < 2; q++) {
             const PllJob& j = jobs.p[k].j[q];
@@ -1098,23 +1055,26 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
             split = split && j.in_neg;
         }
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
-    const int tab_ok = (tab_bytes <= 64 * 1024 && !pll_notab_env()) ? 1 : 0;
+    const int tab_ok = (tab_bytes <= 64 * 1024 && !SDR_PLL_NOTAB) ? 1 : 0;
     const dim3 g(cdiv(split ? 2 * nch : nch, 64), 2), b(64);
     *waves = g.x * g.y;
+    const size_t lds = tab_ok ? tab_bytes : 0;
     // every wave of a persistent launch must be resident at once (a wave that cannot start holds up
-    // the done count of every block, and the producer of later blocks waits for that): at most
-    // max_cus x what fits one CU (the LDS table, one wave per SIMD)
+    // the done count of every block, and the producer of later blocks waits for that): at most the
+    // stream's CUs x the workgroups of this kernel that fit one CU (its VGPRs, the LDS table)
     if (max_cus > 0) {
-        const int per_cu = std::min(4, tab_ok ? (int)(160 * 1024 / tab_bytes) : 4);
-        if ((int)*waves > max_cus * per_cu)
-            return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit %d CUs x %d resident waves: use sdr_plls",
-                        *waves, max_cus, per_cu);
+        const void* kern = vec ? (split ? (const void*)k_pll_multi<true, true> : (const void*)k_pll_multi<true, false>)
+                               : (split ? (const void*)k_pll_multi<false, true> : (const void*)k_pll_multi<false, false>);
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds) != hipSuccess || per_cu <= 0)
+            per_cu = std::min(4, tab_ok ? (int)(160 * 1024 / tab_bytes) : 4);   // one wave per SIMD, the LDS table
+        if ((long long)*waves > (long long)max_cus * per_cu)
+            return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit the stream's %d CUs x %d resident waves "
+                        "(use sdr_plls, or a stream over more CUs)", *waves, max_cus, per_cu);
     }
-    const char* acq = std::getenv("SDR_PLL_ACQUIRE");   // diagnosis: system-scope acquire
-    const int sys_acq = (acq && std::strcmp(acq, "system") == 0) ? 1 : 0;
 #define KPM(V, SP)                                                                                       \
     hipLaunchKernelGGL((k_pll_multi<V, SP>), g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks, words, \
-                       pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc, sys_acq)
+                       pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc)
     if (vec) { if (split) KPM(true, true); else KPM(true, false); }
     else { if (split) KPM(false, true); else KPM(false, false); }
 #undef KPM

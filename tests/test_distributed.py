@@ -171,16 +171,54 @@ class _OracleStepper:
         return None
 
 
-def _bench_worker(rank: int, port: int, q):
+class _PendingStepper(_OracleStepper):
+    """The oracle stepper declaring what the GPU stepper declares with a persistent PLL: a launch is
+    pending from each begin_phase to the phase's synchronize (bench.LaunchWindow guards that span),
+    and a prime_gather round before the first phase. Records the order of the rank path's calls."""
+
+    launch_pending = True
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.log = []
+
+    def prime_gather(self, gather):
+        self.log.append("prime")
+        z = self.outputs_spec()
+        res = gather(lr=torch.zeros(z["lr"][0], dtype=z["lr"][1]), bits=torch.zeros(z["bits"][0], dtype=z["bits"][1]))
+        assert (res is None) == (dist.get_rank() != 0)
+
+    def begin_phase(self, n):
+        self.log.append(f"begin {n}")
+
+    def step(self, b, gather=None):
+        self.log.append(f"step {b}")
+        super().step(b, gather)
+
+    def synchronize(self):
+        self.log.append("sync")
+
+
+class _CollectiveInWindowStepper(_PendingStepper):
+    """Misbehaves: a barrier inside the timed phase's pending-launch window."""
+
+    def step(self, b, gather=None):
+        super().step(b, gather)
+        if b == 3:
+            dist.barrier()
+
+
+def _bench_worker(rank: int, port: int, q, factory=None):
     import argparse
     import bench
+    factory = factory or _OracleStepper
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
     args = argparse.Namespace(channels=NCH_PER_RANK, warmup=2, steps=NBLOCKS - 2, no_gather=False,
                               no_isolated=True, no_cpu_baseline=True, numerics="exact")
     try:
-        res = bench.run_rank(args, WORLD, rank, 0, stepper_factory=_OracleStepper, backend="gloo")
+        res = bench.run_rank(args, WORLD, rank, 0, stepper_factory=factory, backend="gloo")
         st = _OracleStepper.last
-        q.put((rank, res, st.received, st.steps))
+        q.put((rank, res, st.received, getattr(st, "log", st.steps)))
     except BaseException as e:
         q.put((rank, repr(e), None, None))
         raise
@@ -247,3 +285,57 @@ def test_cpu_baseline_untimed_above_one_gpu():
     import bench
     res = bench.cpu_baseline_leg(argparse.Namespace(), None, timing=False)
     assert res["value"] is None and "N > 1" in res["sample"] and "verified" not in res
+
+
+def _run_bench_ranks(factory):
+    import sys
+    sys.path.insert(0, str(ROOT))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, port, q, factory)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(WORLD):
+        rank, res, received, log = q.get(timeout=240)
+        got[rank] = (res, received, log)
+    for p in procs:
+        p.join(timeout=60)
+    return got, [p.exitcode for p in procs]
+
+
+@pytest.mark.timeout(300)
+def test_bench_rank_path_primes_gather_before_pending_launch():
+    """With a persistent launch per phase (the GPU stepper's default), run_rank does one untimed gather
+    round before the first begin_phase (RCCL's lazy set-up and the capture buffers happen outside any
+    pending launch), and inside each phase's window only the per-step gathers run: the rows gathered
+    to rank 0 still equal a single-process run, block for block."""
+    got, codes = _run_bench_ranks(_PendingStepper)
+    assert codes == [0, 0], got
+    for rank in range(WORLD):
+        res, received, log = got[rank]
+        assert not isinstance(res, str), f"rank {rank} failed: {res}"
+        want = (["prime", "sync", "begin 2", "step 0", "step 1", "sync", "sync", "begin 6"] +
+                [f"step {b}" for b in range(2, NBLOCKS)] + ["sync"])
+        assert log[:len(want)] == want, log
+    res0, received, _ = got[0]
+    assert res0["gathered"]["steps"] == NBLOCKS + 1          # the priming round + one per block-step
+    assert len(received) == NBLOCKS
+    ref = [_channel_outputs(c) for c in range(WORLD * NCH_PER_RANK)]
+    for b in range(NBLOCKS):
+        lr, bits = received[b]
+        for c in range(WORLD * NCH_PER_RANK):
+            assert np.array_equal(lr[c], ref[c][0][b]) and np.array_equal(bits[c], ref[c][1][b]), (b, c)
+
+
+@pytest.mark.timeout(300)
+def test_bench_rank_path_rejects_collective_in_launch_window():
+    """A torch.distributed call other than the per-step gather while a phase's persistent launch is
+    pending (here a barrier in the timed phase) fails the run on every rank instead of stalling the
+    blocking PLL stream (bench.LaunchWindow)."""
+    got, codes = _run_bench_ranks(_CollectiveInWindowStepper)
+    for rank in range(WORLD):
+        res = got[rank][0]
+        assert isinstance(res, str) and "pending persistent PLL launch" in res, (rank, res)
+    assert all(c != 0 for c in codes)

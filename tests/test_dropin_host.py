@@ -120,6 +120,32 @@ def test_error_detection_matches_reference(tmp_path):
     assert seen == {"Sync State Detected", "Still Sync-ed", "Lost Sync", "PI: "}   # every branch exercised
 
 
+def test_parse_matches_reference_on_station_registers(tmp_path):
+    """SURVEY 8(f) f1 on the reference's only real-station vectors: the 56 recorded RDS group
+    registers of /root/reference/test/parser_test.cpp:79-136 (PI 0xC27A) through the drop-in parse
+    (host/rds_frame.cpp) print exactly what the reference program's own parse
+    (src/rds_utilities.cpp:172-199, compiled unmodified in oracle/_ref) prints -- PI, PTY "Rock", the
+    Program Service names "  Love  " and "  Dies  " -- and leave the same decoder state.
+    Fixture: tests/golden/make_parser_golden.py."""
+    import base64
+    import json
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = tmp_path / "parse_regs"
+    subprocess.run([gxx, "-O1", "-std=c++17", "-I", str(ROOT / "include" / "dropin"),
+                    str(ROOT / "tests" / "cpp" / "parse_regs_driver.cpp"),
+                    str(ROOT / "real-time-sdr_amd" / "host" / "rds_frame.cpp"), "-o", str(exe)], check=True)
+    fx = json.loads((ROOT / "tests" / "golden" / "golden_parser_regs.json").read_text())
+    assert len(fx["registers"]) == 56
+    r = subprocess.run([str(exe)], input="".join(f"{v}\n" for v in fx["registers"]).encode(), capture_output=True,
+                       check=True, timeout=60)
+    want = base64.b64decode(fx["stderr_b64"])
+    assert r.stderr == want
+    assert r.stdout.decode().strip() == fx["state"]
+    assert b"PI: c27a" in want and b"Program Service:   Love  " in want and b"Program Service:   Dies  " in want
+
+
 def test_fm_batch_queue_protocol(tmp_path):
     """ThreadSafeQueue<FmBatch*> (the device-resident queue payload, include/dropin/fm_batch.h): the
     reference's push / wait_and_pop / prepare protocol with 2 recycled batches, 1 producer and 2

@@ -422,8 +422,13 @@ def own_queue_stream(pkg, torch_cuda):
 
 
 def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda, own_queue_stream):
-    """A persistent launch whose last block is never signalled ends by itself (bounded wait, 5 s),
-    releases its done counter and reports the error; blocks before it are computed normally."""
+    """A persistent launch whose block 2 is signalled too late (after the 5 s bounded wait) ends by
+    itself and never hands out a block it did not compute: blocks before it come out as in the
+    one-stream pipeline, the late block's post stages write SDR_PCM_POISON audio, NaN rds_clean and
+    nbits = SDR_NBITS_POISONED (include/sdr_amd.h), sdr_plls_report raises, the post calls of that
+    launch's blocks then fail, and sdr_ctx_reset + a new launch recover
+    (/root/reference/include/threadsafequeue.h:24-44: a consumer never sees an unpublished block)."""
+    import time
     torch = torch_cuda
     nch, nb = 8, 3
     iqs = [channel_input(synth, 500 + c, nb) for c in range(nch)]
@@ -436,32 +441,58 @@ def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda, own_qu
     with torch.cuda.stream(torch.cuda.Stream()):
         pipe.plls_launch(nb, stream=s_pll)
         lr = torch.empty(nch, 2 * pipe.info.n_audio, dtype=torch.int16, device="cuda")
-        for b in range(nb - 1):
+        clean = torch.empty(nch, pipe.info.n_rds, dtype=torch.float32, device="cuda")
+
+        def block(b):
             pipe.frontend(d[b])
             pipe.stereo_pre()
             pipe.rds_pre()
             pipe.plls_signal()
             pipe.plls_wait(stream=s_post)
             pipe.stereo_post(lr, stream=s_post)
-            pipe.rds_post(None, bits=False, stream=s_post)
-            s_post.synchronize()   # not torch.cuda.synchronize(): the persistent PLL is still running
+            pipe.rds_post(clean, bits=True, stream=s_post)
+            s_post.synchronize()   # not torch.cuda.synchronize(): the persistent PLL may still run
+
+        for b in range(nb - 1):
+            block(b)
             assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
+        time.sleep(6.5)            # the waves give up on block 2 after 5 s of waiting
+        block(nb - 1)              # signalled too late: the PLL never computes it
+        assert (lr.cpu().numpy() == pkg.SDR_PCM_POISON).all(), "late block: audio not poisoned"
+        assert np.isnan(clean.cpu().numpy()).all(), "late block: rds_clean not poisoned"
+        assert (pipe.nbits.cpu().numpy() == pkg.SDR_NBITS_POISONED).all(), "late block: nbits not poisoned"
         with pytest.raises(pkg.SdrError, match="timed out"):
             pipe.plls_report(stream=s_pll)
-        # the context recovers: the abandoned block's PLL never ran (its state is still block 1's), a
-        # new launch resynchronises the sequence numbers and clears the error word, and block 2 then
-        # comes out as in the one-stream pipeline
+        # recovery: reset the state the poisoned launch left, a new launch, block 0 again
+        pipe.reset()
         pipe.plls_launch(1, stream=s_pll)
-        pipe.frontend(d[nb - 1])
-        pipe.stereo_pre()
-        pipe.rds_pre()
-        pipe.plls_signal()
-        pipe.plls_wait(stream=s_post)
-        pipe.stereo_post(lr, stream=s_post)
-        pipe.rds_post(None, bits=False, stream=s_post)
-        s_post.synchronize()
-        assert np.array_equal(lr.cpu().numpy(), ref["stereo"][nb - 1]), "stereo after recovery"
+        block(0)
+        assert np.array_equal(lr.cpu().numpy(), ref["stereo"][0]), "stereo after recovery"
+        assert np.array_equal(clean.cpu().numpy().view(np.uint32), ref["clean"][0].view(np.uint32))
         assert len(pipe.plls_report(stream=s_pll)) == 1
+    pipe.close()
+
+
+def test_persistent_plls_refuses_pool_stream(pkg, torch_cuda):
+    """sdr_plls_launch only accepts a stream sdr_stream_create_cu_range made (its own hardware
+    queue): a plain torch stream is refused before anything is dispatched."""
+    torch = torch_cuda
+    pipe = pkg.Pipeline(4)
+    with pytest.raises(pkg.SdrError, match="sdr_stream_create_cu_range"):
+        pipe.plls_launch(2, stream=torch.cuda.Stream())
+    torch.cuda.synchronize()   # nothing was launched: a pending launch would hold this for 5 s
+    pipe.close()
+
+
+def test_persistent_plls_refuses_unresident_waves(pkg, torch_cuda, own_queue_stream):
+    """4096 channels = 256 PLL waves, 2 per CU (each holds the 59 KB trigArg table in LDS): they do
+    not fit a 64-CU stream at once, so the launch is refused before any dispatch (round 3 timed out
+    on exactly this configuration)."""
+    torch = torch_cuda
+    pipe = pkg.Pipeline(4096)
+    with pytest.raises(pkg.SdrError, match="do not fit"):
+        pipe.plls_launch(2, stream=own_queue_stream())
+    torch.cuda.synchronize()   # returns at once: nothing is pending
     pipe.close()
 
 
