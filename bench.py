@@ -578,14 +578,16 @@ class LaunchWindow:
     PLL stream is CU-masked, hence blocking: anything that synchronises the device implicitly (a
     collective's set-up, a hipMalloc / hipFree of the caching allocator) would wait for the pending
     launch until its 5 s bound. Inside the window every torch.distributed call but the per-step
-    gather (wrapped by gather()) raises, and a device allocation or free made inside it fails the
-    run at exit (torch.cuda.memory_stats num_device_alloc / num_device_free)."""
+    gather (wrapped by gather()) raises; a device allocation or free made between arm() and check()
+    (torch.cuda.memory_stats num_device_alloc / num_device_free, read outside the timed region:
+    the call itself costs a fraction of a millisecond) fails the run."""
 
     def __init__(self, torch, dist, device, active: bool):
         self.torch, self.dist, self.active = torch, dist, active
         self.device = torch.device(device) if not isinstance(device, str) else torch.device(device)
         self.allow = False
         self.saved = {}
+        self.alloc0 = None
         self.log: list[str] = []
 
     def _alloc_counts(self):
@@ -593,6 +595,20 @@ class LaunchWindow:
             return None
         st = self.torch.cuda.memory_stats(self.device)
         return st.get("num_device_alloc", 0), st.get("num_device_free", 0)
+
+    def arm(self) -> "LaunchWindow":
+        """Before the phase (and its timer): the allocation counters the check compares against."""
+        self.alloc0 = self._alloc_counts() if self.active else None
+        return self
+
+    def check(self) -> None:
+        """After the phase (and its timer): no device allocation or free happened in between."""
+        if self.alloc0 is None:
+            return
+        a1 = self._alloc_counts()
+        if a1 != self.alloc0:
+            raise RuntimeError(f"device memory allocated or freed inside a pending persistent PLL launch "
+                               f"(hipMalloc/hipFree counts {self.alloc0} -> {a1})")
 
     def __enter__(self):
         if not self.active:
@@ -611,7 +627,6 @@ class LaunchWindow:
                                            "(only the per-step gather may run there)")
                     return _fn(*a, **k)
                 setattr(self.dist, name, guarded)
-        self.alloc0 = self._alloc_counts()
         return self
 
     def __exit__(self, et, ev, tb):
@@ -621,10 +636,6 @@ class LaunchWindow:
             setattr(self.dist, name, fn)
         self.saved = {}
         self.log.append("close")
-        a1 = self._alloc_counts()
-        if et is None and self.alloc0 is not None and a1 != self.alloc0:
-            raise RuntimeError(f"device memory allocated or freed inside a pending persistent PLL launch "
-                               f"(hipMalloc/hipFree counts {self.alloc0} -> {a1})")
         return False
 
     def gather(self, fn):
@@ -676,19 +687,21 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
         st.synchronize()
         if world > 1:
             dist.barrier()
-        with LaunchWindow(torch, dist, win_dev, pending) as win:
+        with LaunchWindow(torch, dist, win_dev, pending).arm() as win:
             if hasattr(st, "begin_phase") and args.warmup:
                 st.begin_phase(args.warmup)
             for b in range(args.warmup):
                 st.step(b, win.gather(gather))
             st.synchronize()
+        win.check()
         if world > 1:
             dist.barrier()
         if hasattr(st, "prepare_phase"):
             st.prepare_phase(args.steps)
+        win = LaunchWindow(torch, dist, win_dev, pending).arm()
         st.synchronize()
         t0 = time.perf_counter()
-        with LaunchWindow(torch, dist, win_dev, pending) as win:
+        with win:
             if hasattr(st, "begin_phase"):
                 st.begin_phase(args.steps)
             for b in range(args.warmup, nblocks):
@@ -699,6 +712,7 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
             dist.barrier()
         st.synchronize()
         elapsed = time.perf_counter() - t0
+        win.check()
         if world > 1:
             elapsed = max_over_ranks(torch, dist, elapsed, gdev)
         # ---- outside the timed region: parity of the outputs (every rank checks its own captured
