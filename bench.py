@@ -193,6 +193,10 @@ class GpuStepper:
         # CU-masked stream. A fifth dedicated hardware queue starves the front-end stream: the PLL then
         # idles ~1 ms per 20 blocks waiting for input, 0.714 -> 0.78 ms/step, profiles/r03/drain2_ab.txt)
         self.phase = (0, -1)        # first and last block index of the current phase
+        # SDR_BENCH_FILL_PARTS (default 4, 1 = off): the first block of a persistent phase in that
+        # many sample ranges (sdr_frontend_pre_parts), so the PLL starts on its first range
+        self.fill_parts = int(os.environ.get("SDR_BENCH_FILL_PARTS", "4"))
+        self.parts_block = -1
         self.ev_fork, self.ev_join = torch.cuda.Event(), torch.cuda.Event()
         # SDR_BENCH_PLL=persistent (default): one PLL dispatch per phase (warm-up, timed) that waits
         # for each block's device flag (sdr_plls_launch/_signal/_wait); "dispatch": one sdr_plls
@@ -292,11 +296,17 @@ class GpuStepper:
         if b >= 2:
             s_fe.wait_event(self.post_done[b - 2])
         self.fe_start[b].record(s_fe)
-        pipe.frontend(self.iq[b], stream=s_fe)                # rffrontend.cpp:58-71
-        self.fe_end[b].record(s_fe)
-        pipe.pre(stream=s_fe)                                 # stereo.cpp:74, :80 + rds.cpp:105-116
-        if self.persist:                                      # stereo.cpp:77 + rds.cpp:119
-            pipe.plls_signal(stream=s_fe)
+        if first and self.persist and self.fill_parts > 1:
+            # the pipeline fill: the phase's first block in sample ranges, each published to the
+            # persistent PLL as soon as its front end and pre-PLL FIRs are done
+            pipe.frontend_pre_parts(self.iq[b], self.fill_parts, stream=s_fe)
+            self.parts_block = b
+        else:
+            pipe.frontend(self.iq[b], stream=s_fe)            # rffrontend.cpp:58-71
+            self.fe_end[b].record(s_fe)
+            pipe.pre(stream=s_fe)                             # stereo.cpp:74, :80 + rds.cpp:105-116
+            if self.persist:                                  # stereo.cpp:77 + rds.cpp:119
+                pipe.plls_signal(stream=s_fe)
         self.pre_done[b].record(s_fe)
         if edge_fe:                                           # the rest of the phase's front ends follow it
             s_fe = self.s_fe
@@ -306,6 +316,7 @@ class GpuStepper:
             torch.index_select(self.mono, 0, self.vsel, out=self.cap_mono[b])
         if self.persist:
             pipe.plls_wait(stream=s_post)
+            self.pll_done[b].record(s_post)                   # the PLL's block b released (drain timing)
         else:
             s_pll.wait_event(self.pre_done[b])
             self.pll_start[b].record(s_pll)
@@ -379,7 +390,9 @@ class GpuStepper:
         """Kernel-level timings of the timed blocks (HIP events on the launching streams)."""
         info, nch = self.info, self.nch
         rng = range(warmup, self.nblocks)
-        fe_avg_s = float(np.mean([self.fe_start[b].elapsed_time(self.fe_end[b]) for b in rng])) / 1e3
+        # the front end's own launch time; a block whose front end ran in parts (the fill) has none
+        fe_avg_s = float(np.mean([self.fe_start[b].elapsed_time(self.fe_end[b]) for b in rng
+                                  if b != self.parts_block])) / 1e3
         fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
         cyc = None
         timeline = None
@@ -396,12 +409,15 @@ class GpuStepper:
                 idle = sum(max(0, ts[j] - te[j - 1]) for j in range(1, len(ts))) * 1e-5
                 first, last = warmup, warmup + steps - 1
                 phase = self.fe_start[first].elapsed_time(self.post_done[last])
-                fill = self.fe_start[first].elapsed_time(self.pre_done[first])
+                # drain: from the release of the PLL's last block (the post stream's wait) to the end
+                # of its post stage; fill: the rest of the device phase before the PLL span (the
+                # first block's front end and pre-PLL FIRs up to the PLL's first published range)
+                drain = self.pll_done[last].elapsed_time(self.post_done[last])
                 timeline = {"pll_span_ms": round(span, 4), "pll_idle_ms": round(idle, 4),
                             "outside_span_ms": round(elapsed * 1e3 - span, 4),
-                            "device_phase_ms": round(phase, 4), "fill_ms": round(fill, 4),
-                            "fill_frontend_ms": round(self.fe_start[first].elapsed_time(self.fe_end[first]), 4),
-                            "drain_ms": round(phase - fill - span, 4)}
+                            "device_phase_ms": round(phase, 4), "fill_ms": round(phase - span - drain, 4),
+                            "fill_parts": self.fill_parts if self.parts_block == first else 1,
+                            "drain_ms": round(drain, 4)}
         else:
             pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
         achieved = fe_bytes / fe_avg_s / 1e9

@@ -183,6 +183,13 @@ int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
  * launch itself only enqueues the kernel. Ignored by a launch with another nblocks. */
 int sdr_plls_prepare(sdr_ctx *ctx, int nblocks, void *stream);
 int sdr_plls_signal(sdr_ctx *ctx, void *stream);
+/* The pipeline fill: the FIRST block of a pending persistent launch as sdr_frontend + sdr_pre +
+ * sdr_plls_signal in `nparts` sample ranges (at most one per 2048-sample pre-PLL FIR tile), each
+ * range published as soon as its front end and pre-PLL FIRs are done, so the PLLs start on the
+ * block's first range while the rest is produced (the reference's producer hands a block over whole,
+ * threadsafequeue.h:24-44; the PLL consumes its input in order, pll.cpp:34-53, and waits before
+ * every sample that is not published yet). Exact numerics, rds_on, 101 taps only. */
+int sdr_frontend_pre_parts(sdr_ctx *ctx, const uint8_t *iq, size_t iq_stride, int nparts, void *stream);
 int sdr_plls_wait(sdr_ctx *ctx, void *stream);
 int sdr_plls_report(sdr_ctx *ctx, double *block_ms, int max_blocks, int *nblocks, void *stream);
 /* The raw device stamps of the last persistent launch (100 MHz s_memrealtime ticks), per block:

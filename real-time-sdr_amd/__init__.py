@@ -94,6 +94,7 @@ def lib() -> C.CDLL:
         "sdr_plls_launch": ([vp, i32, vp], i32),
         "sdr_plls_prepare": ([vp, i32, vp], i32),
         "sdr_plls_signal": ([vp, vp], i32),
+        "sdr_frontend_pre_parts": ([vp, vp, sz, i32, vp], i32),
         "sdr_plls_wait": ([vp, vp], i32),
         "sdr_plls_report": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32), vp], i32),
         "sdr_plls_cycles": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), vp], i32),
@@ -336,6 +337,12 @@ class Pipeline:
 
     def plls_signal(self, stream=None):
         check(lib().sdr_plls_signal(self._h, _stream(stream)), "sdr_plls_signal")
+
+    def frontend_pre_parts(self, iq, nparts: int, stream=None):
+        """The first block of a pending persistent launch: frontend + pre + plls_signal in nparts
+        sample ranges, each published to the PLLs as soon as it is ready (the pipeline fill)."""
+        check(lib().sdr_frontend_pre_parts(self._h, _ptr(iq), _row_stride(iq), nparts, _stream(stream)),
+              "sdr_frontend_pre_parts")
 
     def plls_wait(self, stream=None):
         check(lib().sdr_plls_wait(self._h, _stream(stream)), "sdr_plls_wait")

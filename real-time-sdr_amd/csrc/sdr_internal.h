@@ -30,9 +30,7 @@ constexpr int DEC_STATE = 8;     // ints of RDS decoder state per channel
 // MFMA front end (sdr_frontend.hip): digit planes of the fixed-point taps and tap fragments
 constexpr int FT_ND = 4;
 constexpr int FT_AFRAGS = 4 * FT_ND;
-constexpr int FT_NB_DEFAULT = 32;
-// exact front end v3 (k_frontend3): outputs per lane segment
-constexpr int FE3_R = 12;
+constexpr int FT_NB = 32;        // 16-output blocks per wave tile
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -101,15 +99,14 @@ struct FrontendArgs {
     int nch, ntaps, block_iq, block_if, D;
     const float* h;            // plain taps (generic kernel)
     const float* hs;           // register-blocked tap table (k_frontend2)
-    const float* hv;           // the 101 taps / 128 as 51 pairs (+ a zero), k_frontend2 with SDR_FE_VTAP
-    const float* hs3;          // the same for k_frontend3's FE3_R outputs per lane (nullptr: not built)
     const void* afrag;         // MFMA tap fragments (fast mode)
     double yscale;             // MFMA fixed-point scale
     const uint32_t* pad80;     // 64 words of u8 128
-    bool fast, mfma;
-    int fe_r, fe_grid, fe_nb, fe_wpe, cus;
+    bool fast;
 };
-int frontend_launch(const FrontendArgs& a, hipStream_t s);
+// the whole block (jn <= 0) or tiles [j0, j0 + jn) of every channel (exact front end only)
+int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0 = 0, int jn = 0);
+int frontend_tiles(int block_if);   // exact front-end tiles per channel and block
 
 // ---- sdr_pll.hip
 int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s);
@@ -126,11 +123,16 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
 // may already finish the next block) and one shared count would release a block early.
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
-                     hipStream_t s, int max_cus);   // max_cus > 0: fail unless every wave fits max_cus CUs
+                     hipStream_t s, int max_cus,    // max_cus > 0: fail unless every wave fits max_cus CUs
+                     int sub_tile);                 // > 0: the first block's input may come in parts of this many samples
 int launch_flag_store(uint32_t* flag, uint32_t v, hipStream_t s);
 int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStream_t s);
 int diag_pll_counts(unsigned long long* out, int reset);
 constexpr int PLL_WORDS_DONE = 4;      // index of the done ring in the words array
+// words[PLL_WORD_SUB]: the parts of a launch's first block published so far, as launch_base *
+// PLL_SUB_SCALE + FIR tiles (a value no earlier launch can have left behind: no reset needed)
+constexpr int PLL_WORD_SUB = 2;
+constexpr uint32_t PLL_SUB_SCALE = 8;
 constexpr uint32_t PLL_DONE_RING = 16; // waves stay within a few blocks of each other
 constexpr int PLL_WORDS = PLL_WORDS_DONE + (int)PLL_DONE_RING;
 
@@ -144,7 +146,7 @@ struct sdr_ctx {
     sdr_info info{};
     int ntaps = 101;
     // taps (device)
-    float *rf_h = nullptr, *rf_hs = nullptr, *rf_hv = nullptr, *rf_hs3 = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *pilot_band_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
+    float *rf_h = nullptr, *rf_hs = nullptr, *pilot_h = nullptr, *stereo_h = nullptr, *pilot_band_h = nullptr, *rds_h = nullptr, *rds_sq_h = nullptr,
           *rrc_h = nullptr;
     float *audio_pp = nullptr, *rdsbb_pp = nullptr;   // polyphase tables
     int *audio_cnt = nullptr, *rdsbb_cnt = nullptr;
@@ -171,14 +173,9 @@ struct sdr_ctx {
     float2* prev = nullptr;                             // [2][nch]
     sdr_pll_state *st_pll = nullptr, *rds_pll = nullptr;
     int32_t* dec = nullptr;                             // [nch][DEC_STATE]
-    int fe_grid = 0;                                    // front-end workgroups (0: one per tile)
-    int fe_r = 8;                                       // front-end outputs per lane (4 or 8)
     uint32_t* pad80 = nullptr;                          // 64 words of u8 128 (the zero sample)
     void* fe_afrag = nullptr;                           // MFMA front end: tap digit fragments
     double fe_yscale = 0.0;                             // 2^-(F+7): fixed-point taps, x = (u-128)/128
-    bool fe_mfma = false;                               // fast mode runs k_frontend_mfma
-    int fe_nb = sdrk::FT_NB_DEFAULT;                    // MFMA front end: 16-output blocks per tile
-    int fe_wpe = 0;                                     // > 0: persistent register-prefetch MFMA front end
     int cus = 0;                                        // compute units of the device
     int parity = 1;                                     // parity of the current block
     long long block = -1;                               // index of the current block

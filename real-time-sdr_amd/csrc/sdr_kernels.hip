@@ -145,6 +145,7 @@ struct FirRb {
     size_t rx_stride;
     const float* hist2_src;
     const uint32_t* err;       // non-null: poison the outputs (NaN) when *err != 0 (a persistent PLL timeout)
+    int x0;                    // first tile (blockIdx.x + x0): a part of the block (sdr_frontend_pre_parts)
 };
 
 #ifndef SDR_FRB_PK_ASM
@@ -171,7 +172,8 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
     constexpr int T = FRB_T, R = FRB_R;
     __shared__ __attribute__((aligned(16))) float sx[(FRB_W + 3) & ~3];
     const int ch = blockIdx.y, tid = threadIdx.x;
-    const int n0 = blockIdx.x * FRB_TILE;
+    const int xt = (int)blockIdx.x + f.x0;                        // tile of the block
+    const int n0 = xt * FRB_TILE;
     const int m0 = n0 - (T - 1);
     const int W = min(FRB_TILE, ny - n0) + T - 1;
     {
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
             if (i < W) sx[i] = SQUARE ? v[u] * v[u] : v[u];       // rds.cpp:111-113
         }
     }
-    if (NT == 3 && f.hist2_src && blockIdx.x == 0 && tid < HIST)  // y[2]'s history (extended stream)
+    if (NT == 3 && f.hist2_src && xt == 0 && tid < HIST)          // y[2]'s history (extended stream)
         f.y[2][(size_t)ch * f.y_stride[2] + tid - HIST] = f.hist2_src[(size_t)ch * f.y_stride[2] + ny - HIST + tid];
     __syncthreads();
     const int nb = n0 + tid * R;
@@ -1485,23 +1487,9 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     c->rds_on = rds_on ? 1 : 0;
     c->flags = flags;
     {
-        // One tile per workgroup by default: measured as fast as a persistent grid in isolation and
-        // 2.5x faster while the other streams' kernels share the chip (the dispatcher balances).
         int cus = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         c->cus = cus;
-        if (const char* e = std::getenv("SDR_FE_MFMA_WPE")) {    // tuning knob: persistent MFMA, waves per SIMD
-            const int k = std::atoi(e);
-            if (k >= 2 && k <= 4) c->fe_wpe = k;
-        }
-        if (const char* e = std::getenv("SDR_FE_WG_PER_CU")) {   // tuning knob: persistent grid, k per CU
-            const int k = std::atoi(e);
-            if (k >= 0 && cus > 0) c->fe_grid = k * cus;
-        }
-        if (const char* e = std::getenv("SDR_FE_R")) {           // tuning knob: outputs per lane
-            const int k = std::atoi(e);
-            if (k == 4 || k == 8) c->fe_r = k;
-        }
     }
     int r = fill_info(&c->info, nch, mode, c->rds_on);
     if (r) { delete c; return r; }
@@ -1527,9 +1515,9 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
 #define TRY(x) do { int r_ = (x); if (r_) { sdr_ctx_destroy(c); return r_; } } while (0)
     TRY(upload(c, &c->rf_h, rf));
     {
-        // front-end v2 tap table: row S (input sample S of a thread window, R = 8 outputs) holds
+        // exact front-end tap table: row S (input sample S of a thread window, R = 8 outputs) holds
         // h[r*D + 100 - S] / 128 (exact power-of-two scaling) or 0 where that tap does not exist
-        const int R = c->fe_r, D = in.rf_decim, TWIN = (R - 1) * D + T;
+        const int R = 8, D = in.rf_decim, TWIN = (R - 1) * D + T;
         std::vector<float> tt((size_t)TWIN * R, 0.0f);
         for (int S_ = 0; S_ < TWIN; S_++)
             for (int r = 0; r < R; r++) {
@@ -1537,18 +1525,6 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
                 if (k >= 0 && k < T) tt[(size_t)S_ * R + r] = rf[k] * 0.0078125f;
             }
         TRY(upload(c, &c->rf_hs, tt));
-        std::vector<float> hv(((size_t)T + 1) / 2 * 2, 0.0f);
-        for (int k = 0; k < T; k++) hv[k] = rf[k] * 0.0078125f;
-        TRY(upload(c, &c->rf_hv, hv));
-        // the same rows for k_frontend3's FE3_R outputs per lane segment
-        const int TW3 = (FE3_R - 1) * D + T;
-        std::vector<float> t3((size_t)TW3 * FE3_R, 0.0f);
-        for (int S_ = 0; S_ < TW3; S_++)
-            for (int r = 0; r < FE3_R; r++) {
-                const int k = r * D + (T - 1) - S_;
-                if (k >= 0 && k < T) t3[(size_t)S_ * FE3_R + r] = rf[k] * 0.0078125f;
-            }
-        TRY(upload(c, &c->rf_hs3, t3));
     }
     if (T == 101 && (in.rf_decim == 10 || in.rf_decim == 4 || in.rf_decim == 3)) {
         // MFMA front end: taps as fixed point h*2^F in FT_ND balanced base-256 digits, laid out as
@@ -1581,8 +1557,6 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
         TRY(upload(c, &dfr, fr));
         c->fe_afrag = dfr;
         c->fe_yscale = std::ldexp(1.0, -(F + 7));
-        c->fe_mfma = std::getenv("SDR_FE_FAST_VALU") == nullptr;   // A/B knob: packed-FMA VALU path
-        if (const char* e = std::getenv("SDR_FE_NB")) c->fe_nb = std::atoi(e);   // tuning knob: 16, 24, 32
     }
     TRY(upload(c, &c->pilot_h, pilot));
     TRY(upload(c, &c->stereo_h, stereo));
@@ -1674,12 +1648,11 @@ int sdr_ctx_info(const sdr_ctx* c, sdr_info* info) {
     return SDR_OK;
 }
 
-int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) {
-    if (!c || !iq) return fail(SDR_E_INVALID, "null argument");
+extern "C++" {
+namespace {
+// the front end's arguments for the block that switches the context to parity p
+FrontendArgs frontend_args(const sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int p) {
     const sdr_info& in = c->info;
-    if (iq_stride < (size_t)2 * in.block_iq || (iq_stride & 1) || (reinterpret_cast<uintptr_t>(iq) & 1))
-        return fail(SDR_E_INVALID, "iq_stride %zu < 2*block_iq %d or misaligned", iq_stride, 2 * in.block_iq);
-    const int p = c->parity ^ 1;
     const int hp = c->ntaps - 1;
     FrontendArgs a{};
     a.iq = iq;
@@ -1698,19 +1671,26 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     a.D = in.rf_decim;
     a.h = c->rf_h;
     a.hs = c->rf_hs;
-    a.hs3 = c->rf_hs3;
-    a.hv = c->rf_hv;
     a.afrag = c->fe_afrag;
     a.yscale = c->fe_yscale;
     a.pad80 = c->pad80;
-    a.fast = (c->flags & SDR_FLAG_FAST_FRONTEND) != 0;
-    a.mfma = c->fe_mfma;
-    a.fe_r = c->fe_r;
-    a.fe_grid = c->fe_grid;
-    a.fe_nb = c->fe_nb;
-    a.fe_wpe = c->fe_wpe;
-    a.cus = c->cus;
-    const int r = frontend_launch(a, S(stream));
+    a.fast = (c->flags & SDR_FLAG_FAST_FRONTEND) != 0 && c->fe_afrag != nullptr;
+    return a;
+}
+int check_iq(const sdr_ctx* c, const uint8_t* iq, size_t iq_stride) {
+    const sdr_info& in = c->info;
+    if (iq_stride < (size_t)2 * in.block_iq || (iq_stride & 1) || (reinterpret_cast<uintptr_t>(iq) & 1))
+        return fail(SDR_E_INVALID, "iq_stride %zu < 2*block_iq %d or misaligned", iq_stride, 2 * in.block_iq);
+    return SDR_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) {
+    if (!c || !iq) return fail(SDR_E_INVALID, "null argument");
+    if (const int r = check_iq(c, iq, iq_stride)) return r;
+    const int p = c->parity ^ 1;
+    const int r = frontend_launch(frontend_args(c, iq, iq_stride, p), S(stream));
     if (r) return r;
     c->parity = p;
     c->block++;
@@ -1762,18 +1742,22 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
 extern "C++" {
 namespace {
 // launch k_fir_rb with NT tap sets (one block of every channel of length n)
+// tiles [x0, x0 + xn) of the block (xn <= 0: all)
 template <int NT, bool SQUARE>
-int fir_rb(const sdr_ctx* c, const float* x, size_t x_stride, int n, const FirRb& f, hipStream_t s) {
+int fir_rb(const sdr_ctx* c, const float* x, size_t x_stride, int n, FirRb f, hipStream_t s, int x0 = 0,
+           int xn = 0) {
+    if (xn <= 0) { x0 = 0; xn = cdiv(n, FRB_TILE); }
+    f.x0 = x0;
     // the 3-set pass with its first two sets as packed pairs
     if constexpr (NT == 3 && !SQUARE) {
         if (f.h01) {
-            hipLaunchKernelGGL((k_fir_rb<3, false, true>), dim3(cdiv(n, FRB_TILE), c->nch), dim3(BLK), 0, s, x,
+            hipLaunchKernelGGL((k_fir_rb<3, false, true>), dim3(xn, c->nch), dim3(BLK), 0, s, x,
                                x_stride, x, x_stride, n, f);
             LAUNCH_CHECK();
             return SDR_OK;
         }
     }
-    hipLaunchKernelGGL((k_fir_rb<NT, SQUARE>), dim3(cdiv(n, FRB_TILE), c->nch), dim3(BLK), 0, s, x, x_stride, x,
+    hipLaunchKernelGGL((k_fir_rb<NT, SQUARE>), dim3(xn, c->nch), dim3(BLK), 0, s, x, x_stride, x,
                        x_stride, n, f);
     LAUNCH_CHECK();
     return SDR_OK;
@@ -1914,7 +1898,7 @@ extern "C++" {
 namespace {
 // squaring (rds.cpp:111-113) + 114 kHz BPF (:116) of the extended rds_band stream -> gen_pilot + its
 // PLL reciprocals
-int rds_sq_fir(sdr_ctx* c, hipStream_t s) {
+int rds_sq_fir(sdr_ctx* c, hipStream_t s, int x0 = 0, int xn = 0) {
     FirRb f{};
     f.h[0] = c->rds_sq_h;
     f.y[0] = c->plain(c->gpilot);
@@ -1922,7 +1906,7 @@ int rds_sq_fir(sdr_ctx* c, hipStream_t s) {
     f.rx0 = c->rxbuf(c->rx_rds);
     f.rx_stride = c->plain_stride;
     f.y0neg = c->plain(c->gpilot_neg);
-    return fir_rb<1, true>(c, c->rband + c->parity * c->fm_par, c->fm_stride, c->info.block_if, f, s);
+    return fir_rb<1, true>(c, c->rband + c->parity * c->fm_par, c->fm_stride, c->info.block_if, f, s, x0, xn);
 }
 }  // namespace
 }  // extern "C++"
@@ -1949,24 +1933,32 @@ int sdr_rds_pre(sdr_ctx* c, void* stream) {
     return SDR_OK;
 }
 
-int sdr_pre(sdr_ctx* c, void* stream) {
-    if (!c) return fail(SDR_E_INVALID, "null context");
-    if (c->block < 0 || c->st_pre_done == c->block || c->rds_pre_done == c->block)
-        return fail(SDR_E_INVALID, "pre: no new block");
-    if (!c->rds_on) return sdr_stereo_pre(c, stream);
-    if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "pre: %d taps", c->ntaps);
-    hipStream_t s = S(stream);
+extern "C++" {
+namespace {
+// pilot, band and RDS band BPFs (stereo.cpp:74,80, rds.cpp:105) from one staged fm_demod window --
+// the third output into the extended rds_band stream, history included -- then the squared 114 kHz
+// BPF; FIR tiles [x0, x0 + xn) of the block (xn <= 0: all)
+int pre_launch(sdr_ctx* c, hipStream_t s, int x0 = 0, int xn = 0) {
     const int n = c->info.block_if, p = c->parity;
-    // pilot, band and RDS band BPFs (stereo.cpp:74,80, rds.cpp:105) from one staged fm_demod window;
-    // the third output goes into the extended rds_band stream, history included
     FirRb f = stereo_fir(c);
     f.h[2] = c->rds_h;
     f.h01 = c->pilot_band_h;
     f.y[2] = c->rband + p * c->fm_par;
     f.y_stride[2] = c->fm_stride;
     f.hist2_src = c->rband + (p ^ 1) * c->fm_par;
-    int r = fir_rb<3, false>(c, c->fm_cur(), c->fm_stride, n, f, s);
-    if (!r) r = rds_sq_fir(c, s);
+    const int r = fir_rb<3, false>(c, c->fm_cur(), c->fm_stride, n, f, s, x0, xn);
+    return r ? r : rds_sq_fir(c, s, x0, xn);
+}
+}  // namespace
+}  // extern "C++"
+
+int sdr_pre(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (c->block < 0 || c->st_pre_done == c->block || c->rds_pre_done == c->block)
+        return fail(SDR_E_INVALID, "pre: no new block");
+    if (!c->rds_on) return sdr_stereo_pre(c, stream);
+    if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "pre: %d taps", c->ntaps);
+    const int r = pre_launch(c, S(stream));
     if (r) return r;
     c->st_pre_done = c->rds_pre_done = c->block;
     return SDR_OK;
@@ -2092,7 +2084,7 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     }
     uint32_t waves = 0;
     const int r = launch_pll_multi(jobs, n, nch, nblocks, c->pers_words, c->pers_launched, c->pers_t0, c->pers_t1,
-                                   c->pers_cyc, &waves, s, scus);
+                                   c->pers_cyc, &waves, s, scus, FRB_TILE);
     if (r) return r;
     c->pers_failed = false;   // this launch's error word was cleared by its prepare
     c->pers_waves = waves;
@@ -2104,24 +2096,65 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     return SDR_OK;
 }
 
+extern "C++" {
+namespace {
+// may `block` be signalled next to the pending persistent launch?
+int plls_signal_check(const sdr_ctx* c, long long block, const char* what) {
+    if (c->pers_signaled == c->pers_launched)
+        return fail(SDR_E_INVALID, "%s: no sdr_plls_launch covers this block", what);
+    // the launch fixed block j's buffer parity as (first block's parity) ^ j: only the blocks that
+    // follow the launch, in order, may be signalled
+    const long long want_block = c->pers_first_block + (long long)(c->pers_signaled - c->pers_base);
+    if (block != want_block)
+        return fail(SDR_E_INVALID, "%s: block %lld, but the launch expects block %lld next", what, block, want_block);
+    // a block's done slot is reused PLL_DONE_RING sequence numbers later: every block must have been
+    // waited for (sdr_plls_wait) before the one that reuses its slot is signalled
+    if (c->pers_signaled - c->pers_waited >= PLL_DONE_RING)
+        return fail(SDR_E_INVALID, "%s: %u blocks signalled but not waited for (at most %u in flight)", what,
+                    c->pers_signaled - c->pers_waited, PLL_DONE_RING);
+    return SDR_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int nparts, void* stream) {
+    if (!c || !iq || nparts < 1) return fail(SDR_E_INVALID, "frontend_pre_parts: bad arguments");
+    if (const int r = check_iq(c, iq, iq_stride)) return r;
+    if (!c->rds_on || c->ntaps != FRB_T || (c->flags & SDR_FLAG_FAST_FRONTEND))
+        return fail(SDR_E_INVALID, "frontend_pre_parts: needs rds_on, 101 taps and the exact front end");
+    if (c->pers_signaled != c->pers_base)
+        return fail(SDR_E_INVALID, "frontend_pre_parts: only the first block of a persistent launch comes in parts");
+    if (const int r = plls_signal_check(c, c->block + 1, "frontend_pre_parts")) return r;
+    hipStream_t s = S(stream);
+    const int n = c->info.block_if, ntiles = cdiv(n, FRB_TILE), fe_tiles = frontend_tiles(n);
+    nparts = std::min(nparts, ntiles);
+    const int p = c->parity ^ 1;
+    const FrontendArgs a = frontend_args(c, iq, iq_stride, p);
+    c->parity = p;                 // the block's buffers (the pre-PLL FIRs read c->parity)
+    c->block++;
+    // part q: the FIR tiles [x0, x1) and the front-end tiles their windows need (tile j writes
+    // outputs [511 j, 511 j + 511)); after each part but the last, the count of published tiles
+    int fe_done = 0;
+    for (int q = 0; q < nparts; q++) {
+        const int x0 = q * ntiles / nparts, x1 = (q + 1) * ntiles / nparts;
+        const int fe_end = q == nparts - 1 ? fe_tiles : std::min(fe_tiles, cdiv(std::min(x1 * FRB_TILE, n), 511));
+        int r = SDR_OK;
+        if (fe_end > fe_done) r = frontend_launch(a, s, fe_done, fe_end - fe_done);
+        fe_done = std::max(fe_done, fe_end);
+        if (!r) r = pre_launch(c, s, x0, x1 - x0);
+        if (!r && q < nparts - 1) r = launch_flag_store(c->pers_words + PLL_WORD_SUB, c->pers_base * PLL_SUB_SCALE + (uint32_t)x1, s);
+        if (r) return r;
+    }
+    c->st_pre_done = c->rds_pre_done = c->block;
+    return sdr_plls_signal(c, stream);   // the whole block: the launch's flag
+}
+
 int sdr_plls_signal(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (c->st_pre_done != c->block || c->rds_pre_done != c->block || c->st_pll_done == c->block ||
         c->rds_pll_done == c->block)
         return fail(SDR_E_INVALID, "plls_signal: run sdr_stereo_pre and sdr_rds_pre on a new block first");
-    if (c->pers_signaled == c->pers_launched)
-        return fail(SDR_E_INVALID, "plls_signal: no sdr_plls_launch covers this block");
-    // the launch fixed block j's buffer parity as (first block's parity) ^ j: only the blocks that
-    // follow the launch, in order, may be signalled
-    const long long want_block = c->pers_first_block + (long long)(c->pers_signaled - c->pers_base);
-    if (c->block != want_block)
-        return fail(SDR_E_INVALID, "plls_signal: block %lld, but the launch expects block %lld next", c->block,
-                    want_block);
-    // a block's done slot is reused PLL_DONE_RING sequence numbers later: every block must have been
-    // waited for (sdr_plls_wait) before the one that reuses its slot is signalled
-    if (c->pers_signaled - c->pers_waited >= PLL_DONE_RING)
-        return fail(SDR_E_INVALID, "plls_signal: %u blocks signalled but not waited for (at most %u in flight)",
-                    c->pers_signaled - c->pers_waited, PLL_DONE_RING);
+    if (const int rc = plls_signal_check(c, c->block, "plls_signal")) return rc;
     const int r = launch_flag_store(c->pers_words, c->pers_signaled + 1u, S(stream));
     if (r) return r;
     c->pers_block = c->block;

@@ -610,9 +610,50 @@ __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx
     t_out = t;
 }
 
+constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrealtime (persistent waits)
+
+// Input gate of the persistent PLL's first block (the pipeline fill, sdr_frontend_pre_parts): the
+// producer publishes the block's input in parts (sub = sub_base + FIR tiles published, each tile
+// `tile` samples) before the whole-block flag; the waves start on the first part and wait before
+// loading samples past what has been published. avail = samples published so far (wave-uniform,
+// scalar): n for every other block, so the check per chunk never waits there.
+struct InGate {
+    const uint32_t* flag;
+    const uint32_t* sub;
+    uint32_t* err;
+    uint32_t want, sub_base;
+    int tile, n, avail;
+    unsigned long long t0;
+};
+
+// samples [0, i_end) must be published: poll (relaxed) the whole-block flag and the part counter,
+// acquire once; bounded like the launch's other waits (an expired wait records the error and lets
+// the wave compute on: the post stages then poison the block)
+__device__ __forceinline__ void gate_wait(InGate& g, int i_end) {
+    if (i_end <= g.avail) return;
+    while (true) {
+        const uint32_t f = __hip_atomic_load(g.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t sb = __hip_atomic_load(g.sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int av = (int32_t)(f - g.want) >= 0 ? g.n : (int)min((int32_t)(sb - g.sub_base), 64) * g.tile;
+        av = __builtin_amdgcn_readfirstlane(min(max(av, 0), g.n));
+        if (av >= i_end) {
+            g.avail = av;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - g.t0 > PLL_WAIT_TICKS) {
+            if (threadIdx.x == 0) __hip_atomic_fetch_or(g.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g.avail = g.n;
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 // pll_run on lane pairs: ch = channel of the pair, xneg = -x row of the producer (lane A's input)
 template <bool VEC, bool TAB>
-__device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, const double* __restrict__ wtab) {
+__device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, const double* __restrict__ wtab,
+                                              InGate* gate = nullptr) {
     const SplitLane L = split_lane();
     const size_t in_stride = jb.in_stride, t_stride = jb.t_stride, out_stride = jb.out_stride;
     sdr_pll_state* __restrict__ st = jb.st;
@@ -655,6 +696,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
         }
     };
     if (nmain > 0) {
+        if (gate) gate_wait(*gate, NB * C);
 #pragma unroll
         for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
     }
@@ -706,6 +748,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
 #pragma unroll
                 for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
             }
+            if (gate) gate_wait(*gate, (min(c0 + u + NB, nmain - 1) + 1) * C);
             load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
         }
     }
@@ -725,6 +768,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
                 wr[k] = TAB ? wtab[i] : 0.0;
             }
         };
+        if (gate) gate_wait(*gate, n);
         if (i_rest < n) load_rest(i_rest);
         for (int i0 = i_rest; i0 < n; i0 += C) {
             float xc[C];
@@ -798,14 +842,14 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
 // clock the launch records an error and completes its remaining blocks without computing, so no
 // wave and no waiting stream can hang.
 // ------------------------------------------------------------------------------------------
-constexpr unsigned long long PLL_WAIT_TICKS = 500000000ull;   // 5 s of s_memrealtime
 
 template <bool VEC, bool SPLIT>
 __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
                                                   const uint32_t* pre_flag, uint32_t pre_first,
                                                   uint32_t* done_ring, uint32_t* err,
                                                   unsigned long long* t_start, unsigned long long* t_end,
-                                                  unsigned long long* t_cyc) {
+                                                  unsigned long long* t_cyc, const uint32_t* sub_flag,
+                                                  uint32_t sub_base, int sub_tile) {
     extern __shared__ double wtab[];
     const int lg = blockIdx.x * blockDim.x + threadIdx.x;
     const int ch = SPLIT ? lg >> 1 : lg;
@@ -814,13 +858,18 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
     bool dead = false;
     for (int j = 0; j < nblocks; j++) {
         const PllJob& jb = jobs.p[j & 1].j[blockIdx.y];   // p[0]: the parity of the launch's first block
+        const uint32_t want = pre_first + (uint32_t)j + 1u;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        // the first block may start on its first published part (SPLIT: the lane-pair PLL gates its
+        // loads, InGate)
+        const bool parts = SPLIT && j == 0 && sub_flag != nullptr;
         if (!dead) {
-            const uint32_t want = pre_first + (uint32_t)j + 1u;
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             // poll with relaxed loads and acquire once: an acquire load at agent scope invalidates
             // the wave's caches (on a multi-XCD device its XCD's L2) on every poll, which slowed the
             // kernels running beside the waiting waves 2-3x
-            while ((int32_t)(__hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+            while ((int32_t)(__hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0 &&
+                   !(parts && (int32_t)(__hip_atomic_load(sub_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                                        sub_base) >= 1)) {
                 __builtin_amdgcn_s_sleep(4);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
                     dead = true;
@@ -847,8 +896,15 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
             }
             if (active) {
                 if (SPLIT) {
-                    if (tab) pll_run_split<VEC, true>(jb, n, ch, wtab);
-                    else pll_run_split<VEC, false>(jb, n, ch, nullptr);
+                    InGate g{pre_flag, sub_flag, err, want, sub_base, sub_tile, n, n, t0};
+                    InGate* gp = nullptr;
+                    if (parts) {
+                        g.avail = 0;
+                        gate_wait(g, 1);      // the part(s) the wait above saw
+                        gp = &g;
+                    }
+                    if (tab) pll_run_split<VEC, true>(jb, n, ch, wtab, gp);
+                    else pll_run_split<VEC, false>(jb, n, ch, nullptr, gp);
                 } else {
                     if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
                     else pll_run<VEC, false>(jb, n, ch, nullptr);
@@ -1043,7 +1099,7 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
 
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
-                     hipStream_t s, int max_cus) {
+                     hipStream_t s, int max_cus, int sub_tile) {
     bool vec = true, split = !SDR_PLL_NOSPLIT;
     for (int k = 0; k < 2; k++)
         for (int q = 0; q < 2; q++) {
@@ -1074,7 +1130,8 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
     }
 #define KPM(V, SP)                                                                                       \
     hipLaunchKernelGGL((k_pll_multi<V, SP>), g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks, words, \
-                       pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc)
+                       pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc, \
+                       sub_tile > 0 ? words + PLL_WORD_SUB : nullptr, pre_first * PLL_SUB_SCALE, sub_tile)
     if (vec) { if (split) KPM(true, true); else KPM(true, false); }
     else { if (split) KPM(false, true); else KPM(false, false); }
 #undef KPM

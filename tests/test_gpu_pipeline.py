@@ -537,54 +537,3 @@ def test_persistent_plls_signal_checks_block_order(pkg, synth, torch_cuda, own_q
             assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
         assert len(pipe.plls_report(stream=s_pll)) == nb - 1
     pipe.close()
-
-
-def _frontend_only(pkg, torch, host, mode, flags):
-    """host: [blk][ch][bytes] u8 -> per-block fm_demod (rows padded to 16 bytes)."""
-    nb, nch, row = host.shape
-    pipe = pkg.Pipeline(nch, mode=mode, rds_on=False, flags=flags)
-    iq = torch.empty(nb, nch, (row + 15) // 16 * 16, dtype=torch.uint8, device="cuda")[:, :, :row]
-    iq.copy_(torch.from_numpy(host))
-    fm = []
-    for b in range(nb):
-        pipe.frontend(iq[b])
-        fm.append(pipe.fm_demod().cpu().numpy().view(np.uint32).copy())
-    pipe.close()
-    return fm
-
-
-@pytest.mark.parametrize("mode", [0, 3])
-def test_frontend_grid_knobs_identical(pkg, synth, oracle, torch_cuda, mode, monkeypatch):
-    """The front end's tuning knobs compute the same bytes as the default grids: the exact
-    register-blocked tile kernel k_frontend2 against the lane-segment kernel k_frontend3
-    (SDR_FE_V3=1, a rejected A/B variant kept bit-exact; mode 0 only, mode 3 runs k_frontend2
-    either way), with several tiles per workgroup
-    (SDR_FE_WG_PER_CU=1: one workgroup per CU): the persistent exact kernel, the persistent LDS-DMA MFMA kernel and the persistent register-prefetch
-    MFMA kernel (SDR_FE_MFMA_WPE), incl. the first block (previous block's tail) and the padding."""
-    import real_time_sdr_amd.synth as s
-    block_iq = oracle.Channel(mode, True).block_iq
-    nb, nch = 3, 67
-    host = np.stack([np.stack([src.next_block(block_iq) for _ in range(nb)])
-                     for src in (s.FMMultiplexSource(300 + c) for c in range(nch))], axis=1)
-    for flags, knobs in ((0, [{"SDR_FE_WG_PER_CU": "1"}, {"SDR_FE_V3": "1"}]),
-                         (pkg.FLAG_FAST_FRONTEND, [{"SDR_FE_WG_PER_CU": "1"},
-                                                   {"SDR_FE_MFMA_WPE": "3", "SDR_FE_WG_PER_CU": "1"},
-                                                   {"SDR_FE_MFMA_WPE": "2"},
-                                                   {"SDR_FE_MFMA_WPE": "3", "SDR_FE_NB": "16",
-                                                    "SDR_FE_WG_PER_CU": "1"}])):
-        for k in ("SDR_FE_WG_PER_CU", "SDR_FE_MFMA_WPE", "SDR_FE_NB", "SDR_FE_V3"):
-            monkeypatch.delenv(k, raising=False)
-        want = _frontend_only(pkg, torch_cuda, host, mode, flags)
-        if flags == 0:
-            ref = [oracle.run_channel(host[:, c], mode, False) for c in (0, nch - 1)]
-            for b in range(nb):
-                for i, c in enumerate((0, nch - 1)):
-                    assert np.array_equal(want[b][c], ref[i]["fm_demod"][b].view(np.uint32))
-        for kv in knobs:
-            for k, v in kv.items():
-                monkeypatch.setenv(k, v)
-            got = _frontend_only(pkg, torch_cuda, host, mode, flags)
-            for k in kv:
-                monkeypatch.delenv(k)
-            for b in range(nb):
-                assert np.array_equal(got[b], want[b]), f"mode {mode} flags {flags} {kv} block {b}"

@@ -39,7 +39,7 @@ def _kinds(synth):
 
 
 KEYS = ("fm", "mono", "lr", "clean", "offset", "nsym", "symbols", "nbits", "bits")
-SCHEDULES = ("dispatch", "persistent")
+SCHEDULES = ("dispatch", "persistent", "persistent_parts")
 
 
 def _check(args):
@@ -91,7 +91,7 @@ def _run_schedule(torch, pkg, bench, iq, dev, schedule: str) -> dict:
     try:
         s_fe, s_pll, s_post, _ = bench.cu_masked_streams(torch, pkg, dev, "64", created)
     except (RuntimeError, AttributeError):
-        if schedule == "persistent":
+        if schedule.startswith("persistent"):
             pytest.skip("no CU-masked streams: the bench does not run the persistent PLL without them")
         s_fe, s_pll, s_post = (torch.cuda.Stream(dev) for _ in range(3))
     E = lambda: torch.cuda.Event()  # noqa: E731
@@ -106,18 +106,26 @@ def _run_schedule(torch, pkg, bench, iq, dev, schedule: str) -> dict:
            "symbols": torch.empty(NBLOCKS, NCH, pkg.SDR_MAX_SYMS, dtype=u8, device=dev),
            "nbits": torch.empty(NBLOCKS, NCH, dtype=i32, device=dev),
            "bits": torch.empty(NBLOCKS, NCH, pkg.SDR_MAX_BITS, dtype=u8, device=dev)}
-    persistent = schedule == "persistent"
+    persistent = schedule.startswith("persistent")
+    parts = 4 if schedule == "persistent_parts" else 0
     if persistent:
         pipe.plls_launch(NBLOCKS, stream=s_pll)
     for b in range(NBLOCKS):                               # bench.GpuStepper.step, outputs captured
         if b >= 2:
             s_fe.wait_event(post_done[b - 2])
-        pipe.frontend(iq[b], stream=s_fe)
-        pipe.fm_demod(cap["fm"][b], stream=s_fe)
-        pipe.mono(cap["mono"][b], stream=s_fe)
-        pipe.pre(stream=s_fe)                              # stereo_pre + rds_pre, one staged window
+        if parts and b == 0:
+            # the pipeline fill: the launch's first block in sample ranges, each published to the PLLs
+            pipe.frontend_pre_parts(iq[b], parts, stream=s_fe)
+            pipe.fm_demod(cap["fm"][b], stream=s_fe)
+            pipe.mono(cap["mono"][b], stream=s_fe)
+        else:
+            pipe.frontend(iq[b], stream=s_fe)
+            pipe.fm_demod(cap["fm"][b], stream=s_fe)
+            pipe.mono(cap["mono"][b], stream=s_fe)
+            pipe.pre(stream=s_fe)                          # stereo_pre + rds_pre, one staged window
+            if persistent:
+                pipe.plls_signal(stream=s_fe)
         if persistent:
-            pipe.plls_signal(stream=s_fe)
             pipe.plls_wait(stream=s_post)
         else:
             pre_done[b].record(s_fe)
