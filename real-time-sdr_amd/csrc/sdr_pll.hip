@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "pll_math.h"
 
@@ -843,19 +844,26 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
 // wave and no waiting stream can hang.
 // ------------------------------------------------------------------------------------------
 
-template <bool VEC, bool SPLIT>
-__global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
-                                                  const uint32_t* pre_flag, uint32_t pre_first,
-                                                  uint32_t* done_ring, uint32_t* err,
-                                                  unsigned long long* t_start, unsigned long long* t_end,
-                                                  unsigned long long* t_cyc, const uint32_t* sub_flag,
-                                                  uint32_t sub_base, int sub_tile) {
+// WG waves per workgroup (1, or 4 to pack one wave per SIMD): the group shares one trigArg table in
+// LDS (all channels of a context advance together, so one table serves every wave whose lanes share
+// the group's trigOffset), its wave 0 polls the block flag, and two barriers per block keep the
+// group's waves on the same block (the table is rebuilt only after every wave finished reading it).
+template <bool VEC, bool SPLIT, int WG>
+__global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
+                                                       const uint32_t* pre_flag, uint32_t pre_first,
+                                                       uint32_t* done_ring, uint32_t* err,
+                                                       unsigned long long* t_start, unsigned long long* t_end,
+                                                       unsigned long long* t_cyc, const uint32_t* sub_flag,
+                                                       uint32_t sub_base, int sub_tile) {
     extern __shared__ double wtab[];
+    __shared__ double sh_toff;
+    __shared__ int sh_dead;
     const int lg = blockIdx.x * blockDim.x + threadIdx.x;
     const int ch = SPLIT ? lg >> 1 : lg;
     const bool active = ch < nch;
+    const bool lane0 = (threadIdx.x & 63) == 0;
     __builtin_amdgcn_s_setprio(3);
-    bool dead = false;
+    bool dead = false;                                 // uniform across the workgroup
     for (int j = 0; j < nblocks; j++) {
         const PllJob& jb = jobs.p[j & 1].j[blockIdx.y];   // p[0]: the parity of the launch's first block
         const uint32_t want = pre_first + (uint32_t)j + 1u;
@@ -867,14 +875,21 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
             // poll with relaxed loads and acquire once: an acquire load at agent scope invalidates
             // the wave's caches (on a multi-XCD device its XCD's L2) on every poll, which slowed the
             // kernels running beside the waiting waves 2-3x
-            while ((int32_t)(__hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0 &&
-                   !(parts && (int32_t)(__hip_atomic_load(sub_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                                        sub_base) >= 1)) {
-                __builtin_amdgcn_s_sleep(4);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
-                    dead = true;
-                    break;
+            if (threadIdx.x < 64) {
+                while ((int32_t)(__hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0 &&
+                       !(parts && (int32_t)(__hip_atomic_load(sub_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                                            sub_base) >= 1)) {
+                    __builtin_amdgcn_s_sleep(4);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
+                        dead = true;
+                        break;
+                    }
                 }
+            }
+            if (WG > 1) {
+                if (threadIdx.x == 0) sh_dead = dead ? 1 : 0;
+                __syncthreads();
+                dead = sh_dead != 0;
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             if (dead && threadIdx.x == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -883,17 +898,23 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
         if (!dead) {
             c0 = __builtin_amdgcn_s_memtime();
             r0 = __builtin_amdgcn_s_memrealtime();
-            if (threadIdx.x == 0)
-                __hip_atomic_fetch_min(t_start + j, r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane0) __hip_atomic_fetch_min(t_start + j, r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const double toff0 = active ? jb.st[ch].trigOffset : 0.0;
             const double w = 2 * 3.14159265358979323846 * (jb.freq / jb.Fs);
-            const double toff_l0 = __shfl(toff0, 0);
-            const bool tab = tab_ok && __all(!active || toff0 == toff_l0) &&
-                             __builtin_fabs(w) * (__builtin_fabs(toff_l0) + (double)n + 1.0) < PLL_TAB_WT_MAX;
-            if (tab) {
-                for (int k = threadIdx.x; k < n; k += 64) wtab[k] = w * (toff_l0 + (double)(k + 1));   // pll.cpp:46-47
+            double toff_g;
+            if (WG == 1) {
+                toff_g = __shfl(toff0, 0);
+            } else {
+                if (threadIdx.x == 0) sh_toff = toff0;
                 __syncthreads();
+                toff_g = sh_toff;
             }
+            const bool group_tab =
+                tab_ok && __builtin_fabs(w) * (__builtin_fabs(toff_g) + (double)n + 1.0) < PLL_TAB_WT_MAX;
+            if (group_tab)
+                for (int k = threadIdx.x; k < n; k += 64 * WG) wtab[k] = w * (toff_g + (double)(k + 1));   // pll.cpp:46-47
+            __syncthreads();
+            const bool tab = group_tab && __all(!active || toff0 == toff_g);
             if (active) {
                 if (SPLIT) {
                     InGate g{pre_flag, sub_flag, err, want, sub_base, sub_tile, n, n, t0};
@@ -912,7 +933,7 @@ __global__ __launch_bounds__(64) void k_pll_multi(const PllJobs2 jobs, int n, in
             }
             __syncthreads();   // every lane's table reads and state/phase stores issued before the release
         }
-        if (threadIdx.x == 0) {
+        if (lane0) {
             if (!dead) {
                 const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
                 __hip_atomic_fetch_max(t_end + j, r1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1112,29 +1133,42 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
         }
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
     const int tab_ok = (tab_bytes <= 64 * 1024 && !SDR_PLL_NOTAB) ? 1 : 0;
-    const dim3 g(cdiv(split ? 2 * nch : nch, 64), 2), b(64);
-    *waves = g.x * g.y;
     const size_t lds = tab_ok ? tab_bytes : 0;
+    const int wave_cnt = cdiv(split ? 2 * nch : nch, 64) * 2;
+    // one wave per workgroup (its own CU time slice and table) while two tables per CU fit the
+    // stream's CUs, else groups of 4 waves -- one per SIMD -- sharing one table per CU
+    const int WG = (max_cus > 0 && wave_cnt > 2 * max_cus) ? 4 : 1;
+    const dim3 g(cdiv(split ? 2 * nch : nch, 64 * WG), 2), b(64 * WG);
+    *waves = g.x * g.y * WG;
+    auto kern_of = [&](auto v, auto sp, auto wg) -> const void* {
+        return reinterpret_cast<const void*>(k_pll_multi<decltype(v)::value, decltype(sp)::value, decltype(wg)::value>);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    using W1 = std::integral_constant<int, 1>;
+    using W4 = std::integral_constant<int, 4>;
+    const void* kern = WG == 4 ? (vec ? (split ? kern_of(T{}, T{}, W4{}) : kern_of(T{}, F{}, W4{}))
+                                      : (split ? kern_of(F{}, T{}, W4{}) : kern_of(F{}, F{}, W4{})))
+                               : (vec ? (split ? kern_of(T{}, T{}, W1{}) : kern_of(T{}, F{}, W1{}))
+                                      : (split ? kern_of(F{}, T{}, W1{}) : kern_of(F{}, F{}, W1{})));
     // every wave of a persistent launch must be resident at once (a wave that cannot start holds up
     // the done count of every block, and the producer of later blocks waits for that): at most the
     // stream's CUs x the workgroups of this kernel that fit one CU (its VGPRs, the LDS table)
     if (max_cus > 0) {
-        const void* kern = vec ? (split ? (const void*)k_pll_multi<true, true> : (const void*)k_pll_multi<true, false>)
-                               : (split ? (const void*)k_pll_multi<false, true> : (const void*)k_pll_multi<false, false>);
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds) != hipSuccess || per_cu <= 0)
-            per_cu = std::min(4, tab_ok ? (int)(160 * 1024 / tab_bytes) : 4);   // one wave per SIMD, the LDS table
-        if ((long long)*waves > (long long)max_cus * per_cu)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WG, lds) != hipSuccess || per_cu <= 0)
+            per_cu = std::min(4 / WG, tab_ok ? (int)(160 * 1024 / tab_bytes) : 4 / WG);
+        if ((long long)g.x * g.y > (long long)max_cus * per_cu)
             return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit the stream's %d CUs x %d resident waves "
-                        "(use sdr_plls, or a stream over more CUs)", *waves, max_cus, per_cu);
+                        "(use sdr_plls, or a stream over more CUs)", *waves, max_cus, per_cu * WG);
     }
-#define KPM(V, SP)                                                                                       \
-    hipLaunchKernelGGL((k_pll_multi<V, SP>), g, b, tab_ok ? tab_bytes : 0, s, jobs, n, nch, tab_ok, nblocks, words, \
-                       pre_first, words + PLL_WORDS_DONE, words + 1, t0, t1, tc, \
-                       sub_tile > 0 ? words + PLL_WORD_SUB : nullptr, pre_first * PLL_SUB_SCALE, sub_tile)
-    if (vec) { if (split) KPM(true, true); else KPM(true, false); }
-    else { if (split) KPM(false, true); else KPM(false, false); }
-#undef KPM
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(PllJobs2, int, int, int, int, const uint32_t*, uint32_t, uint32_t*,
+                                                 uint32_t*, unsigned long long*, unsigned long long*,
+                                                 unsigned long long*, const uint32_t*, uint32_t, int)>(
+                           const_cast<void*>(kern)),
+                       g, b, lds, s, jobs, n, nch, tab_ok, nblocks, words, pre_first, words + PLL_WORDS_DONE,
+                       words + 1, t0, t1, tc, sub_tile > 0 ? words + PLL_WORD_SUB : nullptr,
+                       pre_first * PLL_SUB_SCALE, sub_tile);
     LAUNCH_CHECK();
     return SDR_OK;
 }

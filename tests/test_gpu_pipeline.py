@@ -5,7 +5,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from conftest import channel_input, sha
+from conftest import ROOT, channel_input, sha
 
 pytestmark = pytest.mark.gpu
 
@@ -485,11 +485,12 @@ def test_persistent_plls_refuses_pool_stream(pkg, torch_cuda):
 
 
 def test_persistent_plls_refuses_unresident_waves(pkg, torch_cuda, own_queue_stream):
-    """4096 channels = 256 PLL waves, 2 per CU (each holds the 59 KB trigArg table in LDS): they do
-    not fit a 64-CU stream at once, so the launch is refused before any dispatch (round 3 timed out
-    on exactly this configuration)."""
+    """8192 channels = 512 PLL waves: at most one wave per SIMD (256 VGPRs), four per CU in groups
+    sharing one trigArg table -- 256 waves on a 64-CU stream, so the launch is refused before any
+    dispatch (round 3 timed out on a configuration that did not fit: 4096 channels with one table
+    per wave)."""
     torch = torch_cuda
-    pipe = pkg.Pipeline(4096)
+    pipe = pkg.Pipeline(8192)
     with pytest.raises(pkg.SdrError, match="do not fit"):
         pipe.plls_launch(2, stream=own_queue_stream())
     torch.cuda.synchronize()   # returns at once: nothing is pending
@@ -536,4 +537,74 @@ def test_persistent_plls_signal_checks_block_order(pkg, synth, torch_cuda, own_q
             s_post.synchronize()
             assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
         assert len(pipe.plls_report(stream=s_pll)) == nb - 1
+    pipe.close()
+
+
+def test_persistent_plls_packed_groups_match_sequential(pkg, synth, torch_cuda):
+    """More PLL waves than two per CU of the PLL stream: the persistent launch packs them in groups of
+    four (one wave per SIMD) sharing one trigArg table per CU (512 channels = 32 waves on an 8-CU
+    stream); audio, rds_clean and RDS bits equal the one-stream pipeline's, block by block."""
+    import ctypes as C
+    import sys
+    sys.path.insert(0, str(ROOT))
+    import bench
+    torch = torch_cuda
+    nch, nb = 512, 4
+    d = bench.make_input(torch, nch, nb, first_channel=700, device=torch.device("cuda", 0))   # distinct channels
+    ref = {"stereo": [], "clean": [], "bits": [], "nbits": []}
+    one = pkg.Pipeline(nch)                         # the one-stream pipeline on the same bytes
+    for b in range(nb):
+        one.frontend(d[b])
+        ref["stereo"].append(one.stereo().cpu().numpy())
+        ref["clean"].append(one.rds().cpu().numpy())
+        ref["bits"].append(one.bits.cpu().numpy().copy())
+        ref["nbits"].append(one.nbits.cpu().numpy().copy())
+    one.close()
+    L = pkg.lib()
+    L.sdr_stream_create_cu_range.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int]
+    L.sdr_stream_destroy.argtypes = [C.c_void_p]
+    handles = []
+    for lo, n, exclude in ((0, 8, 0), (0, 8, 1), (0, 8, 1)):   # PLL on CUs [0, 8), the rest elsewhere
+        h = C.c_void_p()
+        assert L.sdr_stream_create_cu_range(C.byref(h), torch.cuda.current_device(), lo, n, exclude) == 0
+        handles.append(h.value)
+    s_pll, s_fe, s_post = (torch.cuda.ExternalStream(h) for h in handles)
+    pipe = pkg.Pipeline(nch)
+    info = pipe.info
+    lr = [torch.empty(nch, 2 * info.n_audio, dtype=torch.int16, device="cuda") for _ in range(2)]
+    clean = torch.empty(nch, info.n_rds, dtype=torch.float32, device="cuda")
+    got = {"stereo": [], "clean": [], "bits": [], "nbits": []}
+    post = [torch.cuda.Event() for _ in range(nb)]
+    with torch.cuda.stream(torch.cuda.Stream()):    # nothing on the null stream while the launch waits
+        pipe.plls_launch(nb, stream=s_pll)
+        for b in range(nb):
+            if b >= 2:
+                s_fe.wait_event(post[b - 2])
+            if b == 0:
+                pipe.frontend_pre_parts(d[b], 4, stream=s_fe)    # the fill, with the packed groups
+            else:
+                pipe.frontend(d[b], stream=s_fe)
+                pipe.pre(stream=s_fe)
+                pipe.plls_signal(stream=s_fe)
+            pipe.plls_wait(stream=s_post)
+            pipe.stereo_post(lr[b % 2], stream=s_post)
+            pipe.rds_post(clean, bits=True, stream=s_post)
+            with torch.cuda.stream(s_post):
+                got["stereo"].append(lr[b % 2].clone())
+                got["clean"].append(clean.clone())
+                got["bits"].append(pipe.bits.clone())
+                got["nbits"].append(pipe.nbits.clone())
+            post[b].record(s_post)
+        s_post.synchronize()
+        ms = pipe.plls_report(stream=s_pll)
+    torch.cuda.synchronize()
+    for h in handles:
+        assert L.sdr_stream_destroy(C.c_void_p(h)) == 0
+    assert len(ms) == nb and all(0 < m < 100 for m in ms), ms
+    for b in range(nb):
+        assert np.array_equal(got["stereo"][b].cpu().numpy(), ref["stereo"][b]), f"stereo block {b}"
+        assert np.array_equal(got["clean"][b].cpu().numpy().view(np.uint32), ref["clean"][b].view(np.uint32)), \
+            f"rds_clean block {b}"
+        assert np.array_equal(got["nbits"][b].cpu().numpy(), ref["nbits"][b]), f"nbits block {b}"
+        assert np.array_equal(got["bits"][b].cpu().numpy(), ref["bits"][b]), f"bits block {b}"
     pipe.close()
