@@ -40,7 +40,7 @@ extern "C" {
 
 /* Context flags */
 #define SDR_FLAG_FAST_FRONTEND 0x1  /* FMA front end: fm_demod within 1e-6 rel., not bit-exact */
-#define SDR_FLAG_PLL_LIBM 0x2       /* PLL via per-step f64 libm calls (A/B reference; env SDR_PLL=libm) */
+#define SDR_FLAG_PLL_LIBM 0x2       /* PLL via per-step f64 libm calls (A/B reference) */
 #define SDR_FLAG_KEEP_INTERMEDIATES 0x4  /* post stages store every intermediate row (carrier, stereo_dc,
                                           * ipll) for sdr_ctx_buffer; by default the NCO, mixers and
                                           * resamplers are fused and only the rows' history is stored */

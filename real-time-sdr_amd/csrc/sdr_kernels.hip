@@ -145,6 +145,8 @@ struct FirRb {
     size_t rx_stride;
     const float* hist2_src;
     const uint32_t* err;       // non-null: poison the outputs (NaN) when *err != 0 (a persistent PLL timeout)
+    float* ydup;               // non-null: y[0] stored here too (stride ydup_stride)
+    size_t ydup_stride;
     int x0;                    // first tile (blockIdx.x + x0): a part of the block (sdr_frontend_pre_parts)
 };
 
@@ -338,6 +340,18 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
 #pragma unroll
             for (int j = 0; j < R; j++)
                 if (nb + j < ny) o[j] = a[t][j];
+        }
+    }
+    if (f.ydup) {                                                 // a second copy of y[0]
+        float* o = f.ydup + (size_t)ch * f.ydup_stride + nb;
+        if (nb + R <= ny) {
+#pragma unroll
+            for (int j = 0; j < R; j += 4)
+                reinterpret_cast<float4*>(o + j)[0] = make_float4(a[0][j], a[0][j + 1], a[0][j + 2], a[0][j + 3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < R; j++)
+                if (nb + j < ny) o[j] = a[0][j];
         }
     }
     if (f.y0neg) {                                                // y[0] feeds a PLL: -y[0]
@@ -882,7 +896,10 @@ struct RdsMix {
     float ncoScale, phaseAdjust;
     float* rdc;                 // this parity's rds_dc, extended (history copied by tile 0)
     const float* rdc_prev;
-    int n;
+    float* rfilt;               // this parity's rds_filt, extended: its history is copied by tile 0 too
+    const float* rfilt_prev;
+    size_t rf_stride;
+    int n, n_rds;
 };
 
 __global__ __launch_bounds__(BLK) void k_rds_mix(const RdsMix a) {
@@ -900,8 +917,11 @@ __global__ __launch_bounds__(BLK) void k_rds_mix(const RdsMix a) {
         a.car[(size_t)ch * a.car_stride + a.n] = cl;
         a.st[ch].lastCarrier = cl;
     }
-    if (blockIdx.x == 0 && threadIdx.x < HIST)
+    if (blockIdx.x == 0 && threadIdx.x < HIST) {
         y[(int)threadIdx.x - HIST] = a.rdc_prev[(size_t)ch * a.fm_stride + a.n - HIST + threadIdx.x];
+        a.rfilt[(size_t)ch * a.rf_stride + (int)threadIdx.x - HIST] =
+            a.rfilt_prev[(size_t)ch * a.rf_stride + a.n_rds - HIST + threadIdx.x];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2261,7 +2281,11 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         a.phaseAdjust = 0.0f;
         a.rdc = rdc;
         a.rdc_prev = c->rdc + (p ^ 1) * c->fm_par;
+        a.rfilt = rfilt;                            // the resampler's history (below)
+        a.rfilt_prev = c->rfilt + (p ^ 1) * c->rf_par;
+        a.rf_stride = c->rf_stride;
         a.n = n;
+        a.n_rds = in.n_rds;
         hipLaunchKernelGGL(k_rds_mix, dim3(cdiv(n + 1, BLK), c->nch), dim3(BLK), 0, s, a);
         LAUNCH_CHECK();
     } else {
@@ -2275,11 +2299,11 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride,
                            c->pllbuf(c->ipll), c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
         LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rfilt, c->rfilt + (p ^ 1) * c->rf_par,
+                           c->rf_stride, in.n_rds);
+        LAUNCH_CHECK();
     }
-    // 247/640 resampler (:130) into the extended rds_filt stream
-    hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rfilt, c->rfilt + (p ^ 1) * c->rf_par,
-                       c->rf_stride, in.n_rds);
-    LAUNCH_CHECK();
+    // 247/640 resampler (:130) into the extended rds_filt stream (history: k_rds_mix / k_hist_copy above)
     if (resample_lc_span(c->rdsbb_L, 247, 640) > 64 * RLC_XL || ((c->rdsbb_L + 3) & ~3) > 64 * RLC_HL)
         return fail(SDR_E_INVALID, "rds_post: resampler tile does not fit (L = %d)", c->rdsbb_L);
     dim3 gr(cdiv(in.n_rds, RLC_TN), cdiv(c->nch, 64));
@@ -2288,22 +2312,18 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
                        c->fm_stride, -HIST, c->rdsbb_pp, c->rdsbb_cnt, c->rdsbb_L, c->rds_ptq, in.n_rds, c->nch,
                        rfilt, c->rf_stride);
     LAUNCH_CHECK();
-    // RRC (:133)
-    float* dst = rds_clean ? rds_clean : c->rds_clean;
-    const size_t dst_stride = rds_clean ? rds_stride : c->clean_stride;
+    // RRC (:133) into the context's rds_clean (sdr_rds_bits reads it) and the caller's buffer
     if (T != FRB_T) return fail(SDR_E_INVALID, "rds_post: %d taps", T);
     {
         FirRb f{};
         f.h[0] = c->rrc_h;
-        f.y[0] = dst;
-        f.y_stride[0] = dst_stride;
+        f.y[0] = c->rds_clean;
+        f.y_stride[0] = c->clean_stride;
+        f.ydup = rds_clean;
+        f.ydup_stride = rds_stride;
         f.err = c->post_err();                      // NaN rows after a persistent PLL timeout
         const int r = fir_rb<1, false>(c, rfilt, c->rf_stride, in.n_rds, f, s);
         if (r) return r;
-    }
-    if (rds_clean) {
-        HIP_TRY(hipMemcpy2DAsync(c->rds_clean, c->clean_stride * sizeof(float), rds_clean, rds_stride * sizeof(float),
-                                 in.n_rds * sizeof(float), c->nch, hipMemcpyDeviceToDevice, s));
     }
     c->rds_dsp_done = c->block;
     return SDR_OK;

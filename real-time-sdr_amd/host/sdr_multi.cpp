@@ -221,20 +221,32 @@ void rf_thread(Shared* sh) {
     hipStream_t s = plain_stream(), s_copy = plain_stream();
     uint8_t* d_iq[2] = {};
     hipEvent_t h2d[2] = {new_event(), new_event()}, fe_done[2] = {new_event(), new_event()};
-    hipEvent_t c0[2] = {timing_event(), timing_event()}, c1[2] = {timing_event(), timing_event()};
+    // copy timing: a ring of event pairs, read without blocking the producer (a pair is waited for
+    // only when the ring wraps onto a copy that has not finished)
+    constexpr int TR = 8;
+    hipEvent_t c0[TR], c1[TR];
+    for (int i = 0; i < TR; i++) { c0[i] = timing_event(); c1[i] = timing_event(); }
+    long long timed = 0;                                    // blocks whose copy time is in h2d_ms
+    auto harvest = [&](long long upto, bool wait) {
+        for (; timed < upto; timed++) {
+            const int t = (int)(timed % TR);
+            if (!wait && hipEventQuery(c1[t]) == hipErrorNotReady) break;
+            sh->h2d_ms += elapsed_ms(c0[t], c1[t]);
+        }
+    };
     for (auto& p : d_iq) check_hip(hipMalloc(reinterpret_cast<void**>(&p), bytes), "hipMalloc");
     Reader rd(o.in, bytes);
     for (long long b = 0;; b++) {
         const int slot = rd.next();
         if (slot < 0) break;
         const int k = (int)(b & 1);
-        if (b >= 2) {
-            check_hip(hipStreamWaitEvent(s_copy, fe_done[k], 0), "hipStreamWaitEvent");
-            sh->h2d_ms += elapsed_ms(c0[k], c1[k]);         // block b-2's copy (long done)
-        }
-        check_hip(hipEventRecord(c0[k], s_copy), "hipEventRecord");
+        if (b >= 2) check_hip(hipStreamWaitEvent(s_copy, fe_done[k], 0), "hipStreamWaitEvent");
+        harvest(b - TR + 1, true);                          // the ring slot this block reuses
+        harvest(b, false);
+        const int t = (int)(b % TR);
+        check_hip(hipEventRecord(c0[t], s_copy), "hipEventRecord");
         check_hip(hipMemcpyAsync(d_iq[k], rd.slot[slot], bytes, hipMemcpyHostToDevice, s_copy), "hipMemcpyAsync");
-        check_hip(hipEventRecord(c1[k], s_copy), "hipEventRecord");
+        check_hip(hipEventRecord(c1[t], s_copy), "hipEventRecord");
         check_hip(hipEventRecord(h2d[k], s_copy), "hipEventRecord");
         rd.release(slot, s_copy);
         check_hip(hipStreamWaitEvent(s, h2d[k], 0), "hipStreamWaitEvent");
@@ -251,8 +263,7 @@ void rf_thread(Shared* sh) {
     }
     sh->q.push(nullptr);                                    // end of stream
     check_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
-    for (long long b = std::max(0LL, sh->blocks - 2); b < sh->blocks; b++)
-        sh->h2d_ms += elapsed_ms(c0[b & 1], c1[b & 1]);
+    harvest(sh->blocks, true);
     sh->read_s = rd.read_s;
     for (auto& p : d_iq) (void)hipFree(p);
     sdr_ctx_destroy(ctx);
@@ -460,15 +471,16 @@ int main(int argc, char** argv) {
     const double signal_s = (double)sh.blocks * sh.info.block_iq / (double)sh.info.rf_Fs;
     const double in_gb = (double)sh.blocks * o.nch * 2.0 * sh.info.block_iq / 1e9;
     const double steady_samples = (double)(sh.blocks - 1) * o.nch * sh.info.block_iq;
+    char after0[128] = "after block 0 n/a (fewer than 2 blocks)";
+    if (sh.blocks >= 2 && steady > 0)
+        std::snprintf(after0, sizeof(after0), "after block 0 %.1f MS/s (%.1fx real time)", steady_samples / steady / 1e6,
+                      (double)(sh.blocks - 1) * sh.info.block_iq / (double)sh.info.rf_Fs / steady);
     std::fprintf(stderr,
-                 "sdr_multi: %d channels x %lld blocks in %.3f s: %.1f MS/s I/Q, %.1fx real time; after block 0 "
-                 "%.1f MS/s (%.1fx real time); input read %.3f s (%.1f GB/s), H2D %.3f s GPU time (%.1f GB/s), "
-                 "L/R D2H %.3f s\n",
-                 o.nch, sh.blocks, sec, samples / sec / 1e6, sec > 0 ? signal_s / sec : 0.0,
-                 steady > 0 ? steady_samples / steady / 1e6 : 0.0,
-                 steady > 0 ? (double)(sh.blocks - 1) * sh.info.block_iq / (double)sh.info.rf_Fs / steady : 0.0, sh.read_s,
-                 sh.read_s > 0 ? in_gb / sh.read_s : 0.0, sh.h2d_ms / 1e3, sh.h2d_ms > 0 ? in_gb / (sh.h2d_ms / 1e3) : 0.0,
-                 sh.d2h_ms / 1e3);
+                 "sdr_multi: %d channels x %lld blocks in %.3f s: %.1f MS/s I/Q, %.1fx real time; %s; "
+                 "input read %.3f s (%.1f GB/s), H2D %.3f s GPU time (%.1f GB/s), L/R D2H %.3f s\n",
+                 o.nch, sh.blocks, sec, sec > 0 ? samples / sec / 1e6 : 0.0, sec > 0 ? signal_s / sec : 0.0, after0,
+                 sh.read_s, sh.read_s > 0 ? in_gb / sh.read_s : 0.0, sh.h2d_ms / 1e3,
+                 sh.h2d_ms > 0 ? in_gb / (sh.h2d_ms / 1e3) : 0.0, sh.d2h_ms / 1e3);
     for (auto& fb : batches) (void)hipFree(fb.d_fm);
     return 0;
 }
