@@ -107,6 +107,7 @@ struct FrontendArgs {
 // the whole block (jn <= 0) or tiles [j0, j0 + jn) of every channel (exact front end only)
 int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0 = 0, int jn = 0);
 int frontend_tiles(int block_if);   // exact front-end tiles per channel and block
+int frontend_tab_r();               // outputs per lane of the exact front end (tap-table row length)
 
 // ---- sdr_pll.hip
 int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s);

@@ -1535,10 +1535,11 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
 #define TRY(x) do { int r_ = (x); if (r_) { sdr_ctx_destroy(c); return r_; } } while (0)
     TRY(upload(c, &c->rf_h, rf));
     {
-        // exact front-end tap table: row S (input sample S of a thread window, R = 8 outputs) holds
-        // h[r*D + 100 - S] / 128 (exact power-of-two scaling) or 0 where that tap does not exist
-        const int R = 8, D = in.rf_decim, TWIN = (R - 1) * D + T;
-        std::vector<float> tt((size_t)TWIN * R, 0.0f);
+        // exact front-end tap table: row S (input sample S of a thread window, R outputs) holds
+        // h[r*D + 100 - S] / 128 (exact power-of-two scaling) or 0 where that tap does not exist;
+        // 32 zero floats past the last row (whole 128-byte tap batches are loaded)
+        const int R = frontend_tab_r(), D = in.rf_decim, TWIN = (R - 1) * D + T;
+        std::vector<float> tt((size_t)TWIN * R + 32, 0.0f);
         for (int S_ = 0; S_ < TWIN; S_++)
             for (int r = 0; r < R; r++) {
                 const int k = r * D + (T - 1) - S_;
@@ -2153,11 +2154,13 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
     c->parity = p;                 // the block's buffers (the pre-PLL FIRs read c->parity)
     c->block++;
     // part q: the FIR tiles [x0, x1) and the front-end tiles their windows need (tile j writes
-    // outputs [511 j, 511 j + 511)); after each part but the last, the count of published tiles
+    // outputs [adv j, adv j + adv), adv = 64 R - 1); after each part but the last, the count of
+    // published tiles
+    const int fe_adv = 64 * frontend_tab_r() - 1;
     int fe_done = 0;
     for (int q = 0; q < nparts; q++) {
         const int x0 = q * ntiles / nparts, x1 = (q + 1) * ntiles / nparts;
-        const int fe_end = q == nparts - 1 ? fe_tiles : std::min(fe_tiles, cdiv(std::min(x1 * FRB_TILE, n), 511));
+        const int fe_end = q == nparts - 1 ? fe_tiles : std::min(fe_tiles, cdiv(std::min(x1 * FRB_TILE, n), fe_adv));
         int r = SDR_OK;
         if (fe_end > fe_done) r = frontend_launch(a, s, fe_done, fe_end - fe_done);
         fe_done = std::max(fe_done, fe_end);

@@ -651,8 +651,10 @@ __device__ __forceinline__ void gate_wait(InGate& g, int i_end) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
-// pll_run on lane pairs: ch = channel of the pair, xneg = -x row of the producer (lane A's input)
-template <bool VEC, bool TAB>
+// pll_run on lane pairs: ch = channel of the pair, xneg = -x row of the producer (lane A's input).
+// GATE: the input arrives in parts (*gate); a separate instantiation, so the blocks that need no
+// gate run the loop without its checks
+template <bool VEC, bool TAB, bool GATE = false>
 __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, const double* __restrict__ wtab,
                                               InGate* gate = nullptr) {
     const SplitLane L = split_lane();
@@ -697,7 +699,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
         }
     };
     if (nmain > 0) {
-        if (gate) gate_wait(*gate, NB * C);
+        if (GATE) gate_wait(*gate, NB * C);
 #pragma unroll
         for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
     }
@@ -749,7 +751,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
 #pragma unroll
                 for (int k = 0; k < C; k++) tb[i0 + k] = tv[k];
             }
-            if (gate) gate_wait(*gate, (min(c0 + u + NB, nmain - 1) + 1) * C);
+            if (GATE) gate_wait(*gate, (min(c0 + u + NB, nmain - 1) + 1) * C);
             load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
         }
     }
@@ -769,7 +771,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
                 wr[k] = TAB ? wtab[i] : 0.0;
             }
         };
-        if (gate) gate_wait(*gate, n);
+        if (GATE) gate_wait(*gate, n);
         if (i_rest < n) load_rest(i_rest);
         for (int i0 = i_rest; i0 < n; i0 += C) {
             float xc[C];
@@ -917,15 +919,15 @@ __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int 
             const bool tab = group_tab && __all(!active || toff0 == toff_g);
             if (active) {
                 if (SPLIT) {
-                    InGate g{pre_flag, sub_flag, err, want, sub_base, sub_tile, n, n, t0};
-                    InGate* gp = nullptr;
                     if (parts) {
-                        g.avail = 0;
+                        InGate g{pre_flag, sub_flag, err, want, sub_base, sub_tile, n, 0, t0};
                         gate_wait(g, 1);      // the part(s) the wait above saw
-                        gp = &g;
+                        if (tab) pll_run_split<VEC, true, true>(jb, n, ch, wtab, &g);
+                        else pll_run_split<VEC, false, true>(jb, n, ch, nullptr, &g);
+                    } else {
+                        if (tab) pll_run_split<VEC, true>(jb, n, ch, wtab);
+                        else pll_run_split<VEC, false>(jb, n, ch, nullptr);
                     }
-                    if (tab) pll_run_split<VEC, true>(jb, n, ch, wtab, gp);
-                    else pll_run_split<VEC, false>(jb, n, ch, nullptr, gp);
                 } else {
                     if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
                     else pll_run<VEC, false>(jb, n, ch, nullptr);
