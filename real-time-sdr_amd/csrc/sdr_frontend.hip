@@ -112,18 +112,9 @@ __global__ __launch_bounds__(BLK) void k_frontend(
 #define SDR_FE_CVT_MID 0   // 1: conversion between the products (more hazard wait states: not adopted)
 #endif
 constexpr int FE_PF = SDR_FE_PF;   // tap rows prefetched this many samples ahead (rotating SGPR ring)
-#ifndef SDR_FE_V4
-#define SDR_FE_V4 0
-#endif
-#ifndef SDR_FE4_R
-#define SDR_FE4_R 12
-#endif
-#ifndef SDR_FE4_TPW
-#define SDR_FE4_TPW 5
-#endif
-// exact front end: outputs per lane (k_frontend2: 16 halves the occupancy, 1.54x slower,
-// profiles/r04/ab_fe_r16.txt; k_frontend4 keeps its next window in registers instead)
-constexpr int FE_R = SDR_FE_V4 ? SDR_FE4_R : 8;
+// exact front end: outputs per lane (16 halves the occupancy: 1.54x slower, profiles/r04/ab_fe_r16.txt;
+// 12 or 16 with the next tile's window prefetched in registers: slower too, profiles/r04/ab_fe_v4.txt)
+constexpr int FE_R = 8;
 // {h, h} * m with h one half (HI) of an SGPR pair: v_pk_mul_f32 with a scalar operand whose half
 // is broadcast to both lanes by op_sel / op_sel_hi (no VGPR copy of the tap)
 __device__ __forceinline__ f32x2 fe_mul_v(double hpair, int hi, f32x2 m) {
@@ -359,216 +350,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     }
 }
 
-#ifndef SDR_FE_BATCH
-#define SDR_FE_BATCH 0
-#endif
-// The register-blocked FIR of the exact front end with every scalar-memory and LDS load issued by
-// hand, a batch ahead: batch q (FB samples, descending) finds its tap rows (FB x R taps, two
-// s_load_dwordx16) and window chunks already in registers; its loads for batch q + 1 go out at its
-// start and one s_waitcnt lgkmcnt(0) closes it. (Compiler-placed waits become lgkmcnt(0) right
-// after a tap load, since scalar loads return out of order: the full scalar-load latency per wait.)
-// win: this lane's window in LDS (TWIN u8 I/Q pairs, 16-byte aligned); hs: the tap table, row S =
-// the R taps sample S meets (rows past TWIN - 1 readable: the table is padded).
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-template <int R, int D, int TWIN>
-__device__ __forceinline__ void fe_fir_batched(const uint8_t* win, const float* __restrict__ hs, f32x2 (&acc)[R]) {
-    constexpr int FB = R == 8 ? 4 : 2;                // rows per batch: FB * R <= 32 taps
-    static_assert(R % 2 == 0 && FB * R <= 32, "a batch is at most 32 taps (two s_load_dwordx16)");
-    constexpr int NT = 101, HP = NT - 1;
-    constexpr int NQ = (TWIN + FB - 1) / FB;
-    constexpr int TCH = (2 * TWIN + 15) / 16;         // 16-byte chunks of the lane window
-    // LDS byte address of this lane's window (addrspace cast: the low 32 bits of the flat address)
-    const uint32_t lw = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint8_t*)win;
-    int zero = 0;
-    asm volatile("" : "+s"(zero));
-    const float* hb = hs + __builtin_amdgcn_readfirstlane(zero);
-    f32x16 tb[2][2];
-    u32x4v ck[TCH];
-    auto first_q = [](int c) { return (TWIN - 1 - (8 * c + 7 < TWIN ? 8 * c + 7 : TWIN - 1)) / FB; };
-    auto lo_of = [](int q) { return TWIN - FB * (q + 1) > 0 ? TWIN - FB * (q + 1) : 0; };   // lowest row of batch q
-    auto tload = [&](f32x16 (&d)[2], int q) {
-        asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(d[0]) : "s"(hb), "s"(lo_of(q) * R * 4) : "memory");
-        asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(d[1]) : "s"(hb), "s"(lo_of(q) * R * 4 + 64) : "memory");
-    };
-    auto cload = [&](int c) {
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ck[c]) : "v"(lw), "i"(16 * c) : "memory");
-    };
-    // batch 0's taps and chunks
-    tload(tb[0], 0);
-#pragma unroll
-    for (int c = TCH - 1; c >= 0; c--)
-        if (first_q(c) == 0) cload(c);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("" : "+s"(tb[0][0]), "+s"(tb[0][1]));
-#pragma unroll
-    for (int c = TCH - 1; c >= 0; c--)
-        if (first_q(c) == 0) asm volatile("" : "+v"(ck[c]));
-    auto sample = [&](int S) -> f32x2 {
-        const u32x4v c4 = ck[S >> 3];
-        const uint32_t w = c4[(S & 7) >> 1] ^ 0x80808080u;
-        return (S & 1) ? fe_cvt_v<1>(w) : fe_cvt_v<0>(w);
-    };
-#pragma unroll
-    for (int q = 0; q < NQ; q++) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (q + 1 < NQ) {
-            tload(tb[(q + 1) & 1], q + 1);
-#pragma unroll
-            for (int c = TCH - 1; c >= 0; c--)
-                if (first_q(c) == q + 1) cload(c);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const int lo = lo_of(q);
-        f32x2 m = sample(TWIN - 1 - FB * q);
-#pragma unroll
-        for (int S = TWIN - 1 - FB * q; S >= lo; S--) {
-            const int row = S - lo;                     // within the batch
-            f32x2 prod[R];
-#pragma unroll
-            for (int r = 0; r < R; r += 2) {
-                const int e = row * R + r;
-                const f32x16& tr = tb[q & 1][e >> 4];
-                const double hp = __builtin_bit_cast(double, f32x2{tr[e & 15], tr[(e & 15) + 1]});
-                if (r * D + HP - S >= 0 && r * D + HP - S < NT) prod[r] = fe_mul_v(hp, 0, m);
-                if ((r + 1) * D + HP - S >= 0 && (r + 1) * D + HP - S < NT) prod[r + 1] = fe_mul_v(hp, 1, m);
-            }
-            const f32x2 m_next = (S > lo) ? sample(S - 1) : m;
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int k = r * D + HP - S;
-                if (k >= 0 && k < NT) acc[r] = fe_add_v(acc[r], prod[r]);   // filter.cpp:115
-            }
-            m = m_next;
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (q + 1 < NQ) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            asm volatile("" : "+s"(tb[(q + 1) & 1][0]), "+s"(tb[(q + 1) & 1][1]));
-#pragma unroll
-            for (int c = TCH - 1; c >= 0; c--)
-                if (first_q(c) == q + 1) asm volatile("" : "+v"(ck[c]));
-        }
-    }
-}
-
-// Exact front end v4: a workgroup (one wave) sweeps up to TPW consecutive tiles of one channel and
-// fetches tile i + 1's u8 window from HBM into registers while it computes tile i from LDS, so the
-// HBM latency hides behind the FIR instead of needing other resident waves. Tiles as k_frontend2
-// (64*R outputs starting one before the first written, advancing by 64*R - 1): bit-identical outputs.
-template <int R, int D, int TPW>
-__global__ __launch_bounds__(64) void k_frontend4(
-    const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
-    uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
-    const float* __restrict__ hs, int block_iq, int block_if,
-    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int j0, int jn,
-    const uint32_t* __restrict__ pad) {
-    constexpr int NT = 101, HP = NT - 1, NTH = 64;
-    constexpr int TILE = NTH * R;
-    constexpr int ADV = TILE - 1;
-    constexpr int WIN = (TILE - 1) * D + NT;          // staged samples (u8 I/Q pairs)
-    constexpr int TWIN = (R - 1) * D + NT;            // samples one lane reads
-    constexpr int NG = (2 * WIN + 3) / 4;             // dwords of one tile window
-    constexpr int PER = (NG + NTH - 1) / NTH;         // dwords per lane
-    constexpr int LDS_BYTES = ((2 * WIN + 15) / 16) * 16 + 32;
-    __shared__ __attribute__((aligned(16))) uint8_t sw[LDS_BYTES];
-    const int t = threadIdx.x;
-    const int gpc = (jn + TPW - 1) / TPW;             // workgroups per channel
-    const int ch = (int)blockIdx.x / gpc, g = (int)blockIdx.x - ch * gpc;
-    const int ja = j0 + g * TPW, jb = min(ja + TPW, j0 + jn);
-    const uint8_t* src = iq + (size_t)ch * iq_stride;
-    const uint8_t* tin = tail_in + (size_t)ch * 2 * HP;
-    float* out = fm + (size_t)ch * fm_stride;
-    // tile j's window -> registers (lane t: dwords t, t + 64, ...); samples before the block from
-    // the previous block's tail, past its end u8 128 (pad)
-    uint32_t pf[PER];
-    auto fetch = [&](int j) {
-        const int m0 = (j * ADV - 1) * D - HP;
-        if (D % 2 == 0 && m0 >= 0 && m0 + WIN <= block_iq) {
-            const uint32_t* gw = reinterpret_cast<const uint32_t*>(src + 2 * m0);
-#pragma unroll
-            for (int k = 0; k < PER; k++) {
-                const int i = t + NTH * k;
-                pf[k] = (k < PER - 1 || i < NG) ? __builtin_nontemporal_load(gw + i) : 0u;
-            }
-        } else if (D % 2 == 0) {
-            const uint32_t* gs = reinterpret_cast<const uint32_t*>(src);
-            const uint32_t* gt = reinterpret_cast<const uint32_t*>(tin);
-#pragma unroll
-            for (int k = 0; k < PER; k++) {
-                const int mm = m0 + 2 * (t + NTH * k);
-                const uint32_t* pa = mm >= 0 ? (mm < block_iq ? gs + (mm >> 1) : pad)
-                                             : (mm >= -HP ? gt + ((HP + mm) >> 1) : pad);
-                pf[k] = *pa;
-            }
-        } else {
-            const uint16_t* s16 = reinterpret_cast<const uint16_t*>(src);
-            const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tin);
-#pragma unroll
-            for (int k = 0; k < PER; k++) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int m = m0 + 2 * (t + NTH * k) + h;
-                    const uint16_t* pa = m >= 0 ? s16 + m : t16 + (HP + m);
-                    if (m < -HP || m >= block_iq) pa = reinterpret_cast<const uint16_t*>(pad);
-                    v |= (uint32_t)*pa << (16 * h);
-                }
-                pf[k] = v;
-            }
-        }
-    };
-    if (ja < jb) fetch(ja);
-    for (int j = ja; j < jb; j++) {
-        const int c0 = j * ADV - 1;                   // first decimated output (the carry)
-        {
-            uint32_t* sd = reinterpret_cast<uint32_t*>(sw);
-#pragma unroll
-            for (int k = 0; k < PER; k++) {
-                const int i = t + NTH * k;
-                if (k < PER - 1 || i < NG) sd[i] = pf[k];
-            }
-        }
-        __syncthreads();
-        if (j + 1 < jb) fetch(j + 1);                 // in flight during this tile's FIR
-        f32x2 acc[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
-        fe_fir_batched<R, D, TWIN>(sw + 2 * t * R * D, hs, acc);
-        // ---- discriminator (demod.cpp:8-19); the previous output of lane t's first comes from t-1
-        const f32x2 left = f32x2{__shfl_up(acc[R - 1].x, 1), __shfl_up(acc[R - 1].y, 1)};
-        const int cbase = c0 + t * R;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const int c = cbase + r;
-            f32x2 pv = (r > 0) ? acc[r > 0 ? r - 1 : 0] : left;
-            if (c == 0) {
-                const float2 p = prev_in[ch];
-                pv = f32x2{p.x, p.y};
-            }
-            const f32x2 cur = acc[r];
-            float v;
-            if ((cur.x == 0) & (cur.y == 0)) {
-                v = 0.0f;
-            } else {
-                const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
-                const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
-                v = (float)((double)num / den);
-            }
-            if (c > c0 && c >= 0 && c < block_if) out[c] = v;
-            if (c == block_if - 1) prev_out[ch] = make_float2(cur.x, cur.y);
-        }
-        if (j == 0) {
-            const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);
-            uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
-            for (int i = t; i < HP; i += NTH) tout[i] = last[i];
-            const float* o = fm_other + (size_t)ch * fm_stride;
-            for (int i = t; i < HIST; i += NTH) out[i - HIST] = o[block_if - HIST + i];
-        }
-        __syncthreads();                              // the window is read before the next overwrites it
-    }
-}
-
 // Exact front end, one tile per workgroup (64 lanes): a tile = 64*R decimated outputs starting one
 // before the first fm_demod sample it writes (the discriminator's carry, demod.cpp:16); tiles
 // advance by 64*R-1. The tile's u8 window goes HBM -> registers (coalesced dwords) -> LDS, then every
@@ -647,16 +428,13 @@ __global__ __launch_bounds__(64) void k_frontend2(
     }
     __syncthreads();
     // ---- FIR: R outputs per thread, samples in descending order ----
-    f32x2 acc[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
-#if SDR_FE_BATCH
-    fe_fir_batched<R, D, TWIN>(sw + 2 * t * R * D, hs, acc);
-#else
     uint4 chunk[TCH];
     const uint4* tw = reinterpret_cast<const uint4*>(sw + 2 * t * R * D);
     chunk[TCH - 1] = tw[TCH - 1];
     if (TCH >= 2) chunk[TCH - 2] = tw[TCH - 2];
+    f32x2 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
     // Taps live in SGPRs: row S of the table holds the R taps sample S meets (uniform across the
     // wave), fetched with scalar loads FE_PF samples ahead into a rotating ring and fed to the packed
     // multiplies as scalar operands (op_sel picks the half of the SGPR pair), so the VALU gets its
@@ -708,7 +486,6 @@ __global__ __launch_bounds__(64) void k_frontend2(
         }
         __builtin_amdgcn_sched_barrier(0);
     }
-#endif
     // ---- discriminator (demod.cpp:8-19); the previous output of lane t's first comes from t-1
     const f32x2 left = f32x2{__shfl_up(acc[R - 1].x, 1), __shfl_up(acc[R - 1].y, 1)};
     float* out = fm + (size_t)ch * fm_stride;
@@ -769,17 +546,9 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0, int jn) {
     if (jn <= 0) { j0 = 0; jn = tiles_ch; }
     if (j0 < 0 || j0 + jn > tiles_ch) return fail(SDR_E_INVALID, "frontend: tiles [%d, %d) of %d", j0, j0 + jn, tiles_ch);
     const dim3 g2(jn * a.nch);
-#if SDR_FE_V4
-    const dim3 g4(cdiv(jn, SDR_FE4_TPW) * a.nch);
-#define FE2(DD)                                                                                            \
-    hipLaunchKernelGGL((k_frontend4<FE_R, DD, SDR_FE4_TPW>), g4, dim3(64), 0, s, iq, iq_stride, tail_in,     \
-                       tail_out, prev_in, prev_out, a.hs, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride, j0, \
-                       jn, a.pad80)
-#else
 #define FE2(DD)                                                                                            \
     hipLaunchKernelGGL((k_frontend2<FE_R, DD>), g2, dim3(64), 0, s, iq, iq_stride, tail_in, tail_out, prev_in, \
                        prev_out, a.hs, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride, j0, jn, a.pad80)
-#endif
     if (a.fast) {
         if (j0 != 0 || jn != tiles_ch) return fail(SDR_E_INVALID, "frontend: parts need the exact front end");
         const v4i* af = static_cast<const v4i*>(a.afrag);
