@@ -105,13 +105,8 @@ __global__ __launch_bounds__(BLK) void k_frontend(
 // sched_barrier closes every sample so the scheduler keeps the sample-major order (ILP across the
 // R accumulators, each product next to its add) instead of hoisting products or serialising one
 // output's chain; the LDS chunk two chunks ahead is read at each chunk boundary.
-#ifndef SDR_FE_PF
-#define SDR_FE_PF 5
-#endif
-#ifndef SDR_FE_CVT_MID
-#define SDR_FE_CVT_MID 0   // 1: conversion between the products (more hazard wait states: not adopted)
-#endif
-constexpr int FE_PF = SDR_FE_PF;   // tap rows prefetched this many samples ahead (rotating SGPR ring)
+constexpr int FE_PF = 5;           // tap rows prefetched this many samples ahead (rotating SGPR ring;
+                                   // 2-8 and hand-issued batches measured, profiles/r02/fe_exact_ab.txt)
 // exact front end: outputs per lane (16 halves the occupancy: 1.54x slower, profiles/r04/ab_fe_r16.txt;
 // 12 or 16 with the next tile's window prefetched in registers: slower too, profiles/r04/ab_fe_v4.txt)
 constexpr int FE_R = 8;
@@ -124,19 +119,11 @@ __device__ __forceinline__ f32x2 fe_mul_v(double hpair, int hi, f32x2 m) {
     return r;
 }
 // (I, Q) of one sample, sign-extended from the bytes of a dword that holds two samples
-// (u8 ^ 0x80 == u8 - 128 as int8), converted in program order (volatile asm)
-#ifndef SDR_FE_CVT_C
-#define SDR_FE_CVT_C 0
-#endif
+// (u8 ^ 0x80 == u8 - 128 as int8), converted in program order (volatile asm; the plain C++ form
+// saves hazard waits but is no faster, profiles/r02/ab_fe_exact_asm.txt, profiles/r04/ab_fe_v4.txt)
 template <int HALF>
 __device__ __forceinline__ f32x2 fe_cvt_v(uint32_t w) {
     f32x2 r;
-#if SDR_FE_CVT_C
-    // plain C++ (the SDWA peephole forms the same sext-byte conversions): no inline-asm hazard
-    r.x = (float)(int)(int8_t)(uint8_t)(w >> (16 * HALF));
-    r.y = (float)(int)(int8_t)(uint8_t)(w >> (16 * HALF + 8));
-    return r;
-#endif
     if (HALF) {
         asm volatile("v_cvt_f32_i32_sdwa %0, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2\n\t"
                      "v_cvt_f32_i32_sdwa %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3"
@@ -148,17 +135,10 @@ __device__ __forceinline__ f32x2 fe_cvt_v(uint32_t w) {
     }
     return r;
 }
-#ifndef SDR_FE_ADD_C
-#define SDR_FE_ADD_C 0
-#endif
 __device__ __forceinline__ f32x2 fe_add_v(f32x2 a, f32x2 b) {
-#if SDR_FE_ADD_C
-    return a + b;   // v_pk_add_f32, ordered by its operands (no inline-asm hazard wait after the products)
-#else
     f32x2 r;
     asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
-#endif
 }
 // ------------------------------------------------------------------------------------------
 // Fast-mode front end on the matrix cores (SDR_FLAG_FAST_FRONTEND): the decimating FIR as an
@@ -182,12 +162,6 @@ __device__ __forceinline__ f32x2 fe_add_v(f32x2 a, f32x2 b) {
 constexpr int ft_adv(int D, int NB) { return D == 3 ? 16 * NB - 8 : 16 * NB - 4; }
 constexpr int ft_carry(int D) { return D == 10 ? 2 : D == 4 ? 1 : 4; }
 constexpr int ft_win(int D, int NB) { return 16 * D * (NB - 1) + 256; }
-#ifndef FT_RECOMB_F64
-#define FT_RECOMB_F64 0
-#endif
-#ifndef FT_CT_UNROLL
-#define FT_CT_UNROLL 1
-#endif
 
 // One wave tile of the MFMA front end, I and Q of a block in ONE lane (NB a multiple of 16): a
 // C tile is 16 blocks, columns = blocks, and the I and Q planes are two MFMA groups with the same A
@@ -207,7 +181,7 @@ __device__ __forceinline__ void ft_tile_iq(const int8_t* __restrict__ lds, const
     // row 4g - 1 of this block (lane t - 16) or row 15 of the previous block (lane 48 + n - 1)
     const int src_lane = g > 0 ? t - 16 : (n > 0 ? t + 47 : t);
     float carry_i = 0.0f, carry_q = 0.0f;             // row 15 of the previous C tile's last block
-#pragma unroll FT_CT_UNROLL
+#pragma unroll 1
     for (int ct = 0; ct < NB / 16; ct++) {
         const int bb = 16 * ct + n;
         v4i aI[FT_ND], aQ[FT_ND];

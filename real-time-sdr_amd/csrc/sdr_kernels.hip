@@ -150,19 +150,6 @@ struct FirRb {
     int x0;                    // first tile (blockIdx.x + x0): a part of the block (sdr_frontend_pre_parts)
 };
 
-#ifndef SDR_FRB_PK_ASM
-#define SDR_FRB_PK_ASM 0
-#endif
-// {h0, h1} * {v, v}: tap sets 0 and 1 of one sample in one packed multiply; the tap pair is an SGPR
-// pair, the sample the low (HI = 0) or high half of a VGPR pair, broadcast to both lanes by op_sel
-template <int HI>
-__device__ __forceinline__ f32x2 frb_pk_mul(double hpair, f32x2 wpair) {
-    f32x2 r;
-    if (HI) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "s"(hpair), "v"(wpair));
-    else asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(r) : "s"(hpair), "v"(wpair));
-    return r;
-}
-
 // PK (NT == 3): tap sets 0 and 1 (the stereo pilot and band BPFs) run as packed pairs -- one
 // v_pk_mul_f32 + one v_pk_add_f32 per sample and output for both, the same two roundings each as
 // filter.cpp:115 -- and set 2 (the RDS BPF) scalar: 4 VALU per sample and output instead of 6.
@@ -241,14 +228,10 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
 #pragma unroll
                     for (int j = 0; j < R; j++) {
                         const int i = j + T - 1 - k;
-#if SDR_FRB_PK_ASM
-                        const f32x2 wp = f32x2{w[i & ~1], w[i | 1]};
-                        const f32x2 pr = (i & 1) ? frb_pk_mul<1>(hp, wp) : frb_pk_mul<0>(hp, wp);
-#else
                         // plain vector code: the compiler broadcasts the sample by op_sel (no copy)
-                        // and knows the packed result's latency (no inline-asm wait state)
+                        // and knows the packed result's latency (no inline-asm wait state, unlike an
+                        // inline-asm v_pk_mul_f32)
                         const f32x2 pr = __builtin_bit_cast(f32x2, hp) * f32x2{w[i], w[i]};
-#endif
                         a01[j] = a01[j] + pr;                                  // filter.cpp:115
                         a2[j] = a2[j] + sb[c & 1][kk] * w[i];
                     }

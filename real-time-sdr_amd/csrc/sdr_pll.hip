@@ -491,11 +491,8 @@ __device__ __forceinline__ SplitLane split_lane() {
 // value of the other lane of the pair (DPP quad_perm [1,0,3,2])
 // (bound_ctrl set: both lanes of a pair are always active, and it lets the compiler fold the move
 // into the consumer as a DPP source, v_mul_f32_dpp)
-#ifndef SDR_PLL_DPP_BC
-#define SDR_PLL_DPP_BC 1
-#endif
 __device__ __forceinline__ float pair_swap(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, SDR_PLL_DPP_BC));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
 }
 __device__ __forceinline__ double pair_swap(double v) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
@@ -539,28 +536,15 @@ __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx
     const float g = xs * pair_swap(r.fb);
     const double q = (double)g * r.f;
     const double base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
-#if SDR_PLL_SPLIT_ED
-    // ed = base + rx qA + rx qB with the own product first: one dependent level less after q, but
-    // the two lanes round in different orders, so each lane proves both ends of its own bracket
-    const double ed = pllm::fma_(pair_swap(q), rx, pllm::fma_(q, rx, base));
-    const float e = (float)ed;
-    pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, (float)(ed - pllm::EPS_ABS_E2)),
-                      __builtin_bit_cast(uint32_t, (float)(ed + pllm::EPS_ABS_E2)));
-    (void)L;
-#else
+    // (ed = base + rx qA + rx qB, own product first, is one dependent level shorter but needs both
+    // bracket ends per lane: 2 instructions more, slower, profiles/r03/ab_pll_split.txt)
     const double Y = q + pair_swap(q);
     const double ed = pllm::fma_(Y, rx, base);
     const float e = (float)ed;                                     // = RN32(atan2) when proven
     pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, (float)(ed + L.eps)), __builtin_bit_cast(uint32_t, e));
-#endif
     pf.emaxf = fmaxf(pf.emaxf, __builtin_fabsf(e));               // f32: two steps per v_max3_f32
-    {   // pll.cpp:41-42
-        float ki_e = Ki * e, kp_e = Kp * e;
-#if SDR_PLL_SPLIT_LF
-        // scalar f32 (5 instructions): the SLP-packed form reads packed-f32 results, and on gfx950 each
-        // such read waits a state (s_nop) on the step's dependent chain
-        asm("" : "+v"(ki_e), "+v"(kp_e));
-#endif
+    {   // pll.cpp:41-42 (scalar f32, this unit is built without SLP: profiles/r03/ab_pll_split3.txt)
+        const float ki_e = Ki * e, kp_e = Kp * e;
         const float integ = r.ip.x + ki_e;
         r.ip.y = (r.ip.y + kp_e) + integ;
         r.ip.x = integ;
@@ -580,31 +564,16 @@ __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx
     r.nq1 = (uint32_t)__builtin_bit_cast(uint64_t, kdp);
     r.b = (uint32_t)(__builtin_bit_cast(uint64_t, rr) >> 63);
     r.mr = -rr;
-    const double z = rr * rr, z2 = z * z;
+    const double z = rr * rr;
     const double u = pllm::fma_(rr, L.k1, L.k0);
-#ifndef SDR_PLL_SPLIT_POLY
-#define SDR_PLL_SPLIT_POLY 1   // Horner (profiles/r03/ab_pll_split3.txt)
-#endif
-#if SDR_PLL_SPLIT_POLY == 2
-    // f = (u + zu A01) + zu z^2 (A23 + z^2 A45): one multiply more, one dependent level less
-    const double zu = z * u;
-    const double B = pllm::fma_(z2, pllm::fma_(z, L.c5, L.c4), pllm::fma_(z, L.c3, L.c2));
-    const double Cl = pllm::fma_(zu, pllm::fma_(z, L.c1, L.c0), u);
-    r.f = pllm::fma_(zu * z2, B, Cl);
-#elif SDR_PLL_SPLIT_POLY == 1
-    // Horner: one instruction fewer than Estrin (no z^2), two dependent levels more
-    (void)z2;
+    // Horner: one instruction fewer than Estrin (no z^2), two dependent levels more; faster than
+    // Estrin and than a two-level form (profiles/r03/ab_pll_split3.txt)
     double P = pllm::fma_(z, L.c5, L.c4);
     P = pllm::fma_(z, P, L.c3);
     P = pllm::fma_(z, P, L.c2);
     P = pllm::fma_(z, P, L.c1);
     P = pllm::fma_(z, P, L.c0);
     r.f = pllm::fma_(z * u, P, u);
-#else
-    const double P = pllm::fma_(z2, pllm::fma_(z2, pllm::fma_(z, L.c5, L.c4), pllm::fma_(z, L.c3, L.c2)),
-                                pllm::fma_(z, L.c1, L.c0));
-    r.f = pllm::fma_(z * u, P, u);
-#endif
     r.fb = (float)r.f;                                             // pll.cpp:49-50, reduced frame
     pf.tie = min(pf.tie, pllm::tie_key64(r.f));                   // this lane's rounding (pll_math.h)
     if (!TAB) pf.tmax = fmaxf(pf.tmax, __builtin_fabsf(t));
