@@ -446,7 +446,7 @@ __global__ __launch_bounds__(BLK) void k_resample(const float* __restrict__ xa, 
 // ptq[n] = (q << 8) | phase with phase = nD mod U, q = nD / U (host table; U < 256). Sums stay
 // in ascending j (= ascending k of the reference) as f32 product then f32 add.
 // ------------------------------------------------------------------------------------------
-constexpr int RLC_TN = 32;     // outputs per workgroup (8 per wave)
+constexpr int RLC_TN = 32;     // outputs per workgroup (8 per wave; 16: 218 VGPRs, 2 waves per SIMD)
 constexpr int RLC_XL = 3;      // staged samples per lane and row: 64 * 3 >= the q span + look-back
 constexpr int RLC_HL = 2;      // staged taps per lane and polyphase row: 64 * 2 >= L4
 
@@ -866,7 +866,7 @@ __global__ __launch_bounds__(BLK) void k_poison_i16(const uint32_t* __restrict__
 // ipll[i] in f32 with delay[i] = rds_band[i - 50] + 0 (the APF of :122 is an exact 50-sample
 // shift that turns -0 into +0) into the extended rds_dc stream, history included. ipll itself is
 // not stored: only its last sample (the next block's ipll[0], and pllblock_args.lastCarrier).
-// One thread per IF sample; thread n computes ipll[n].
+// MIX_R samples per thread; the thread whose range holds n computes ipll[n].
 // ------------------------------------------------------------------------------------------
 struct RdsMix {
     const float* rband;         // this parity's rds_band, extended
@@ -885,20 +885,45 @@ struct RdsMix {
     int n, n_rds;
 };
 
+// MIX_R consecutive samples per thread: one 16-byte load of the phases, two 8-byte loads of the
+// delayed band (i - 50 = 2 mod 4), one 16-byte store -- 4x the bytes in flight per wave of the
+// one-sample form, which waited on memory 74 % of its time (profiles/r03/stage_counters_v7.json)
+constexpr int MIX_R = 4;
 __global__ __launch_bounds__(BLK) void k_rds_mix(const RdsMix a) {
     const int ch = blockIdx.y;
-    const int i = blockIdx.x * BLK + threadIdx.x;
+    const int i0 = ((int)blockIdx.x * BLK + (int)threadIdx.x) * MIX_R;
     const float* tt = a.t + (size_t)ch * a.plain_stride;
+    const float* rb = a.rband + (size_t)ch * a.fm_stride;
     float* y = a.rdc + (size_t)ch * a.fm_stride;
-    if (i < a.n) {
-        const float car = (i == 0) ? a.car_prev[(size_t)ch * a.car_stride + a.n]
-                                   : nco_carrier(tt[i - 1], a.ncoScale, a.phaseAdjust);
-        const float d = a.rband[(size_t)ch * a.fm_stride + i - 50] + 0.0f;    // rds.cpp:122
-        y[i] = 2 * d * car;                                                    // rds.cpp:125-127
-    } else if (i == a.n) {
-        const float cl = nco_carrier(tt[a.n - 1], a.ncoScale, a.phaseAdjust);
-        a.car[(size_t)ch * a.car_stride + a.n] = cl;
-        a.st[ch].lastCarrier = cl;
+    auto carrier = [&](int i, float tprev) {
+        return (i == 0) ? a.car_prev[(size_t)ch * a.car_stride + a.n] : nco_carrier(tprev, a.ncoScale, a.phaseAdjust);
+    };
+    if (i0 + MIX_R <= a.n) {
+        const float4 tv = *reinterpret_cast<const float4*>(tt + i0);
+        const float tm = i0 > 0 ? tt[i0 - 1] : 0.0f;
+        const float2 r01 = *reinterpret_cast<const float2*>(rb + i0 - 50);
+        const float2 r23 = *reinterpret_cast<const float2*>(rb + i0 - 48);
+        const float tp[MIX_R] = {tm, tv.x, tv.y, tv.z};
+        const float dl[MIX_R] = {r01.x, r01.y, r23.x, r23.y};
+        float o[MIX_R];
+#pragma unroll
+        for (int k = 0; k < MIX_R; k++) {
+            const float d = dl[k] + 0.0f;                                  // rds.cpp:122
+            o[k] = 2 * d * carrier(i0 + k, tp[k]);                         // rds.cpp:125-127
+        }
+        *reinterpret_cast<float4*>(y + i0) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+        for (int k = 0; k < MIX_R; k++) {
+            const int i = i0 + k;
+            if (i < a.n) {
+                const float d = rb[i - 50] + 0.0f;
+                y[i] = 2 * d * carrier(i, i > 0 ? tt[i - 1] : 0.0f);
+            } else if (i == a.n) {
+                const float cl = nco_carrier(tt[a.n - 1], a.ncoScale, a.phaseAdjust);
+                a.car[(size_t)ch * a.car_stride + a.n] = cl;
+                a.st[ch].lastCarrier = cl;
+            }
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x < HIST) {
         y[(int)threadIdx.x - HIST] = a.rdc_prev[(size_t)ch * a.fm_stride + a.n - HIST + threadIdx.x];
@@ -2272,7 +2297,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         a.rf_stride = c->rf_stride;
         a.n = n;
         a.n_rds = in.n_rds;
-        hipLaunchKernelGGL(k_rds_mix, dim3(cdiv(n + 1, BLK), c->nch), dim3(BLK), 0, s, a);
+        hipLaunchKernelGGL(k_rds_mix, dim3(cdiv(n + 1, BLK * MIX_R), c->nch), dim3(BLK), 0, s, a);
         LAUNCH_CHECK();
     } else {
         {
