@@ -5,6 +5,9 @@ Prints the product kernels (sdrk / anonymous-namespace kernels, not torch's) in 
 start and end relative to the first kernel of the window, their duration and queue, from the
 dispatch of the n-th persistent PLL launch (the timed phase's) on:
   python tools/timeline.py gpurun_out/tr/kernel_trace.csv [--launch 1] [--rows 60]
+  python tools/timeline.py gpurun_out/tr/kernel_trace.csv --by-grid k_frontend2
+(--by-grid: that kernel's average duration per grid size -- whole-block launches apart from the
+pipeline fill's part launches, which a plain --stats average mixes in)
 """
 from __future__ import annotations
 
@@ -22,8 +25,18 @@ def main() -> None:
     ap.add_argument("csv")
     ap.add_argument("--launch", type=int, default=1, help="which k_pll_multi dispatch (0 = warm-up phase)")
     ap.add_argument("--rows", type=int, default=60)
+    ap.add_argument("--by-grid", default=None, metavar="KERNEL")
     args = ap.parse_args()
     rows = [r for r in csv.DictReader(open(args.csv))]
+    if args.by_grid:
+        by: dict[int, list[float]] = {}
+        for r in rows:
+            if args.by_grid in r["Kernel_Name"]:
+                by.setdefault(int(r["Grid_Size_X"]), []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        print(f"{args.by_grid}: grid_size_x  launches  avg_us  min_us  max_us")
+        for g, v in sorted(by.items()):
+            print(f"  {g:>10} {len(v):>9} {sum(v) / len(v):7.1f} {min(v):7.1f} {max(v):7.1f}")
+        return
     ks = []
     for r in rows:
         n = r["Kernel_Name"]
