@@ -36,7 +36,8 @@ host: $(HOSTLIB) $(CLI) $(MULTI)
 # the lane-pair PLL step is faster scalar too (packed-f32 results cost a wait state on gfx950,
 # profiles/r03/ab_pll_split3.txt)
 build/sdr_kernels.hip.o: HIPFLAGS += -fno-slp-vectorize
-build/sdr_pll.hip.o: HIPFLAGS += -fno-slp-vectorize
+build/sdr_pll.hip.o: HIPFLAGS += -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp
+# (the lane-pair PLL step scheduled for ILP: 212.4 -> 210.4 shader cycles per step, profiles/r04/ab_sched.txt)
 
 build/%.o: $(PKG)/csrc/% $(HDRS)
 	@mkdir -p build

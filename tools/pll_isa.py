@@ -23,7 +23,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-gpu-flush-denormals-to-zero",
          "-mllvm", "-pragma-unroll-threshold=1000000", "-fno-slp-vectorize", "-I", str(ROOT / "include"),
-         "--cuda-device-only", "--no-gpu-bundle-output", "-c"]
+         "-mllvm", "-amdgpu-sched-strategy=max-ilp", "--cuda-device-only", "--no-gpu-bundle-output", "-c"]
 F64 = re.compile(r"^v_(fma|fmac|add|mul|cvt_f32_f64|cvt_f64_f32|cvt_f64_i32|fract|rndne)_f64|^v_cvt_f(32|64)_f(64|32)|^v_cvt_f64_i32")
 
 
@@ -53,10 +53,12 @@ def parse(line: str):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
+    ap.add_argument("--extra", default="", help="extra compiler flags (scheduler A/B)")
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
         obj = pathlib.Path(d) / "pll.o"
-        subprocess.run([HIPCC, *FLAGS, "-o", str(obj), str(ROOT / "real-time-sdr_amd/csrc/sdr_pll.hip")], check=True)
+        subprocess.run([HIPCC, *FLAGS, *args.extra.split(), "-o", str(obj), str(ROOT / "real-time-sdr_amd/csrc/sdr_pll.hip")],
+                       check=True)
         dis = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", str(obj)], capture_output=True, text=True,
                              check=True).stdout
     lines = dis.split("\n")
