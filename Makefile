@@ -39,7 +39,7 @@ build/sdr_kernels.hip.o: HIPFLAGS += -fno-slp-vectorize
 build/sdr_pll.hip.o: HIPFLAGS += -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp
 # (the lane-pair PLL step scheduled for ILP: 212.4 -> 210.4 shader cycles per step, profiles/r04/ab_sched.txt)
 
-build/%.o: $(PKG)/csrc/% $(HDRS)
+build/%.o: $(PKG)/csrc/% $(HDRS) Makefile
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
