@@ -1,7 +1,8 @@
 # Build a variant of libsdr_amd.so with extra flags into build/variants/<name>.so, for A/B timing
 # through SDR_AMD_LIB=<path> (tools/gpu/*.sh); per-file flags as in the Makefile.
 #   bash tools/build_variant.sh <name> -DFOO=1 ...
-#   PLLFLAGS="-mllvm ..." bash tools/build_variant.sh <name>    (flags for sdr_pll.hip only)
+#   PLLFLAGS="-mllvm ..." bash tools/build_variant.sh <name>    (flags for sdr_pll.hip only;
+#   FEFLAGS for sdr_frontend.hip, KFLAGS for sdr_kernels.hip)
 set -e
 name=$1; shift
 d=build/variants/$name.obj
@@ -10,7 +11,11 @@ common="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-fl
 pids=""
 for f in sdr_kernels.hip sdr_frontend.hip sdr_pll.hip sdr_taps.cpp; do
   extra=""
-  case $f in sdr_kernels.hip) extra=-fno-slp-vectorize;; sdr_pll.hip) extra="-fno-slp-vectorize ${PLLFLAGS--mllvm -amdgpu-sched-strategy=max-ilp}";; esac
+  case $f in
+    sdr_kernels.hip) extra="-fno-slp-vectorize ${KFLAGS:-}";;
+    sdr_frontend.hip) extra="${FEFLAGS:-}";;
+    sdr_pll.hip) extra="-fno-slp-vectorize ${PLLFLAGS--mllvm -amdgpu-sched-strategy=max-ilp}";;
+  esac
   /opt/rocm/bin/hipcc $common $extra "$@" -c -o $d/$f.o real-time-sdr_amd/csrc/$f & pids="$pids $!"
 done
 for p in $pids; do wait $p; done
