@@ -1,5 +1,5 @@
 # A/B timing of library variants (build/variants/<name>.so, tools/build_variant.sh) on the isolated
-# front end; "default" = the in-tree libsdr_amd.so. VARIANTS="default u2" [ENVS="SDR_FE_NB=32"]
+# front end; "default" = the in-tree libsdr_amd.so. VARIANTS="default u2" [ENVS="NAME=value"]
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-ab}

@@ -1,8 +1,8 @@
 # A/B of library variants on the full bench, interleaved REPS times. A variant is
 #   default          the in-tree libsdr_amd.so
 #   <name>           build/variants/<name>.so (tools/build_variant.sh)
-#   <name>@VAR=val   either of the above with an environment setting (e.g. default@SDR_PLL_TAB=0)
-#   VARIANTS="default nb3 default@SDR_PLL_TAB=0" REPS=2 bash tools/gpu/ab_bench.sh
+#   <name>@VAR=val   either of the above with an environment setting (e.g. default@SDR_BENCH_FILL_PARTS=1)
+#   VARIANTS="default s1 default@SDR_BENCH_FILL_PARTS=1" REPS=2 bash tools/gpu/ab_bench.sh
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-abb}

@@ -1,5 +1,5 @@
 # Isolated front-end A/B over library variants (build/variants/<name>.so; "default" = in-tree lib),
-# interleaved REPS times: VARIANTS="default fepf5" [ENVS="SDR_FE_R=4"] bash tools/gpu/fe_ab.sh
+# interleaved REPS times: VARIANTS="default fepf5" [ENVS="NAME=value"] bash tools/gpu/fe_ab.sh
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-feab}

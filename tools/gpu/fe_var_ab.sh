@@ -1,4 +1,4 @@
-# isolated exact front end over library variants with env settings: VARIANTS="default vtap2@SDR_FE_R=4"
+# isolated exact front end over library variants with env settings: VARIANTS="default feb default@NAME=value"
 set -o pipefail
 O=gpurun_out/${TAG:-fevar}
 mkdir -p $O
