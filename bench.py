@@ -224,6 +224,9 @@ class GpuStepper:
         self.pll_start, self.pll_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
         self.gather_done = [ev() for _ in range(nblocks)]
         self.pre_done, self.post_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
+        # SDR_BENCH_FE_WAIT=post: the front end of block b also waits for block b-2's whole post
+        # stream work (the output copies and captures included), as before the library's own release
+        self.fe_waits_post = os.environ.get("SDR_BENCH_FE_WAIT", "library") == "post"
         # outputs of a few channels, captured on the producing streams for the check after timing
         nv = min(VERIFY_CHANNELS, nch)
         self.vsel = torch.tensor(sorted({int(round(i * (nch - 1) / max(1, nv - 1))) for i in range(nv)}),
@@ -292,8 +295,10 @@ class GpuStepper:
             s_post = self.s_all
             s_post.wait_event(self.post_done[b - 1]) if b >= 1 else None
         # the front end of block b reuses block b-2's parity: both consumers must have released it
-        # (threadsafequeue.h:29-31), i.e. block b-2's post-PLL work is done
-        if b >= 2:
+        # (threadsafequeue.h:29-31). The library orders that itself: sdr_frontend waits on its stream
+        # for the release counts that block b-2's mono, stereo post and RDS mixer stored on theirs
+        # (the RDS chain after its mixer and the output captures are not waited for)
+        if b >= 2 and self.fe_waits_post:
             s_fe.wait_event(self.post_done[b - 2])
         self.fe_start[b].record(s_fe)
         if first and self.persist and self.fill_parts > 1:
@@ -334,9 +339,8 @@ class GpuStepper:
             self.ev_fork.record(s_post)
             s_st.wait_event(self.ev_fork)
         pipe.stereo_post(lr, stream=s_st)                     # stereo.cpp:83-107
-        pipe.rds_post(self.clean, bits=True, stream=s_post)   # rds.cpp:122-167
+        pipe.rds_post(self.clean, bits=True, stream=s_post, bits_out=bits)   # rds.cpp:122-167
         with torch.cuda.stream(s_post):
-            bits.copy_(pipe.bits)
             torch.index_select(bits, 0, self.vsel, out=self.cap_bits[b])
             torch.index_select(pipe.nbits, 0, self.vsel, out=self.cap_nbits[b])
         with torch.cuda.stream(s_st):
@@ -422,6 +426,7 @@ class GpuStepper:
             pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
         achieved = fe_bytes / fe_avg_s / 1e9
         redo = self._pll_redo()
+        waves = self._pll_waves(info.block_if)
         kname = ("k_frontend_mfma" if self.fast else "k_frontend2") + " (u8 I/Q -> 101-tap FIR /10 on I,Q -> FM discriminator)"
         return {
             "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -439,7 +444,8 @@ class GpuStepper:
                     "share_of_step": round(pll_ms / (elapsed / steps * 1e3), 4),
                     **self._pll_issue(cyc),
                     **({"timeline": timeline} if timeline else {}),
-                    **({"chunk_redo": redo} if redo else {})},
+                    **({"chunk_redo": redo} if redo else {}),
+                    **({"waves": waves} if waves else {})},
         }
 
     @staticmethod
@@ -458,6 +464,39 @@ class GpuStepper:
             if "cycles_per_step" in out and pc.get("valu_per_step"):
                 out["issue_frac"] = round(4.0 * pc["valu_per_step"] / out["cycles_per_step"], 4)
         return out
+
+    def _pll_waves(self, n: int) -> dict | None:
+        """Diagnosis builds (-DSDR_PLL_WAVES=1) only: the persistent launch's waves (the timed phase)
+        per job -- mean and slowest shader cycles per step inside their blocks, and the flag-poll
+        time per block -- to tell a slow wave from the hand-off in the span's excess over the mean."""
+        import ctypes as C
+        f = getattr(self.pkg.lib(), "sdr_diag_pll_waves", None)
+        if f is None or not self.persist:
+            return None
+        nmax, nf = 4096, 8
+        c = (C.c_ulonglong * (nf * nmax))()
+        nw = f(c, nmax)
+        if nw <= 0:
+            return None
+        v = np.frombuffer(c, dtype=np.uint64).reshape(nmax, nf)[:nw].astype(np.float64)
+        v = v[(v[:, 3] > 0) & (v[:, 2] > 0)]
+        out = {}
+        for job, name in ((1, "stereo_19k"), (2, "rds_114k")):
+            w = v[v[:, 3] == job]
+            if len(w) == 0:
+                continue
+            cyc = w[:, 0] / w[:, 2] / n
+            poll_us = w[:, 1] / w[:, 2] * 1e-2
+            out[name] = {"waves": int(len(w)), "cycles_per_step_mean": round(float(cyc.mean()), 2),
+                         "cycles_per_step_max": round(float(cyc.max()), 2),
+                         "cycles_per_step_min": round(float(cyc.min()), 2),
+                         "poll_us_per_block_mean": round(float(poll_us.mean()), 2),
+                         "poll_us_per_block_max": round(float(poll_us.max()), 2),
+                         "spin_us_per_block_mean": round(float((w[:, 4] / w[:, 2] * 1e-2).mean()), 2),
+                         "polls_unset_per_block": round(float((w[:, 5] / w[:, 2]).mean()), 2),
+                         "blocks_flag_ready_frac": round(float((w[:, 6] / w[:, 2]).mean()), 3),
+                         "flag_ahead_us_per_block": round(float((w[:, 7] / w[:, 2] * 1e-2).mean()), 2)}
+        return out or None
 
     def _pll_redo(self) -> dict | None:
         """Diagnosis builds (-DSDR_PLL_COUNT=1) only: fraction of the PLL's 16-step chunks whose proof

@@ -367,16 +367,20 @@ class Pipeline:
         check(lib().sdr_plls_cycles(self._h, C.byref(cyc), C.byref(mhz), _stream(stream)), "sdr_plls_cycles")
         return cyc.value, mhz.value
 
-    def rds_post(self, out=None, bits=True, stream=None):
+    def rds_post(self, out=None, bits=True, stream=None, bits_out=None):
+        """bits_out: a [nch][SDR_MAX_BITS] u8 tensor the block's bits go to instead of self.bits."""
         check(lib().sdr_rds_post(self._h, _ptr(out), _row_stride(out) if out is not None else 0, _stream(stream)),
               "sdr_rds_post")
         if bits:
-            self.rds_bits(stream)
+            self.rds_bits(stream, bits_out)
         return out
 
-    def rds_bits(self, stream=None):
+    def rds_bits(self, stream=None, bits_out=None):
+        b = self.bits if bits_out is None else bits_out
+        if tuple(b.shape) != (self.nch, SDR_MAX_BITS) or b.dtype != self.bits.dtype or not b.is_contiguous():
+            raise ValueError(f"bits_out must be a contiguous [{self.nch}][{SDR_MAX_BITS}] uint8 tensor")
         check(lib().sdr_rds_bits(self._h, _ptr(self.offset), _ptr(self.nsym), _ptr(self.symbols), SDR_MAX_SYMS,
-                                 _ptr(self.nbits), _ptr(self.bits), SDR_MAX_BITS, _stream(stream)), "sdr_rds_bits")
+                                 _ptr(self.nbits), _ptr(b), SDR_MAX_BITS, _stream(stream)), "sdr_rds_bits")
 
     def push_fm_demod(self, fm, stream=None):
         """Make fm [nch][block_if] (device f32) the current block (the queue's consumer side)."""

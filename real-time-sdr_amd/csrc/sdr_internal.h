@@ -129,6 +129,7 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
 int launch_flag_store(uint32_t* flag, uint32_t v, hipStream_t s);
 int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStream_t s);
 int diag_pll_counts(unsigned long long* out, int reset);
+int diag_pll_waves(unsigned long long* out, int nmax);
 constexpr int PLL_WORDS_DONE = 4;      // index of the done ring in the words array
 // words[PLL_WORD_SUB]: the parts of a launch's first block published so far, as launch_base *
 // PLL_SUB_SCALE + FIR tiles (a value no earlier launch can have left behind: no reset needed)
@@ -198,6 +199,16 @@ struct sdr_ctx {
     long long pers_block = -1;                          // block of the last signal
     uint32_t pers_block_seq = 0;                        // its sequence number
     hipEvent_t pers_ev = nullptr;                       // orders a prepare on another stream after the last launch
+    // parity release (sdr_kernels.hip release_record / release_wait): rel_words[p][slot] counts the
+    // blocks of parity p read by slot 0 sdr_mono (fm), 1 sdr_stereo_post (fm, band, t_st, carrier),
+    // 2 sdr_rds_post's mixer (rband, t_rds, ipll), stored on the reader's stream (rel_stream) after
+    // its kernels; the producers of the block two later wait for the count on their own streams
+    static constexpr int REL_SLOTS = 3;
+    uint32_t* rel_words = nullptr;                      // [2][REL_SLOTS] counters + 1 timeout word
+    uint32_t rel_seq[2][REL_SLOTS] = {};
+    hipStream_t rel_stream[2][REL_SLOTS] = {};
+    uint32_t rel_waited[2][REL_SLOTS] = {};            // the count a wait on rel_waited_on already covers
+    hipStream_t rel_waited_on[2][REL_SLOTS] = {};
     bool pers_failed = false;                           // sdr_plls_report saw a timeout of the current launch
     // the error word the post stages of the current block check (their outputs are poisoned when a
     // persistent wait timed out): only for blocks signalled through a persistent launch

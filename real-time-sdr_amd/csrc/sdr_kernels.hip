@@ -960,6 +960,27 @@ __global__ __launch_bounds__(BLK) void k_mix(const float* __restrict__ a, size_t
     }
 }
 
+// The parity-release wait (release_wait): every word w[k] with bit k of mask reaches want[k] (counts
+// stored by k_flag_store after the readers' kernels); polled relaxed, acquired once, bounded like the
+// persistent PLL's waits (after ~5 s the wait records 1 in *err and lets the stream go on)
+__global__ void k_rel_wait(const uint32_t* w, uint32_t want0, uint32_t want1, uint32_t want2, unsigned mask,
+                           uint32_t* err) {
+    if (threadIdx.x != 0) return;
+    const uint32_t want[3] = {want0, want1, want2};
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 3; k++) {
+        if (!(mask & (1u << k))) continue;
+        while ((int32_t)(__hip_atomic_load(w + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want[k]) < 0) {
+            __builtin_amdgcn_s_sleep(4);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {
+                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 // copy the previous parity's last HIST samples in front of this parity's stream
 __global__ void k_hist_copy(float* __restrict__ y, const float* __restrict__ y_other, size_t stride, int n) {
     const int ch = blockIdx.x;
@@ -1017,27 +1038,29 @@ __global__ void k_demod_prev(float2* __restrict__ prev, const float* __restrict_
 }
 
 // cdr(), rds_utilities.cpp:4-21: argmax over offsets i < sps of sum_k |(int)x[k*sps+i]|,
-// first maximum wins, 0 when every sum is 0. One wave per channel, one lane per offset.
+// first maximum wins, 0 when every sum is 0. One wave per channel, one lane per offset; the argmax
+// is a wave reduction of (sum, -offset) over the sums > 0 (the reference's strict > from maxv = 0).
 __device__ __forceinline__ int cdr_wave(const float* x, int n, int sps, int* sums) {
+    (void)sums;
     const int lane = threadIdx.x;
     const int nk = n / sps;
-    for (int i = lane; i < sps; i += blockDim.x) {
+    unsigned long long key = 0;                     // (sum << 32) | ~offset of this lane's best offset
+    for (int i = lane; i < sps; i += 64) {
         uint32_t s = 0;
         for (int k = 0; k < nk; k++) {
             const int32_t v = cvt_i32_x86(x[k * sps + i]);
             s += (uint32_t)(v < 0 ? -(uint32_t)v : (uint32_t)v);
         }
-        sums[i] = (int32_t)s;
+        const int32_t si = (int32_t)s;
+        const unsigned long long ki = si > 0 ? ((unsigned long long)(uint32_t)si << 32) | (uint32_t)~(uint32_t)i : 0ull;
+        if (ki > key) key = ki;
     }
-    __syncthreads();
-    int maxi = 0, maxv = 0;
-    for (int i = 0; i < sps; i++) {
-        if (sums[i] > maxv) {
-            maxv = sums[i];
-            maxi = i;
-        }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const unsigned long long o = __shfl_xor(key, m, 64);
+        if (o > key) key = o;
     }
-    return maxi;
+    return key ? (int)~(uint32_t)(key & 0xFFFFFFFFull) : 0;
 }
 
 __global__ __launch_bounds__(64) void k_cdr(int32_t* __restrict__ offset, const float* __restrict__ x,
@@ -1056,9 +1079,9 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
                                                  int32_t* __restrict__ offset_out, int32_t* __restrict__ nsym_out,
                                                  uint8_t* __restrict__ sym_out, size_t sym_stride,
                                                  int32_t* __restrict__ nbits_out, uint8_t* __restrict__ bits_out,
-                                                 size_t bits_stride, const uint32_t* __restrict__ err) {
-    // dynamic LDS: 64 cdr sums, then the channel's whole block (n floats), staged with every load in
-    // flight (the cdr reads it 39-strided and the slicer sps-strided: from LDS, not global memory)
+                                                 size_t bits_stride, const uint32_t* __restrict__ err, int vec4) {
+    // dynamic LDS: 64 ints (unused), then the channel's whole block (n floats), staged with every
+    // load in flight (the cdr reads it 39-strided and the slicer sps-strided: from LDS, not global memory)
     extern __shared__ int sums_dyn[];
     float* xs = reinterpret_cast<float*>(sums_dyn + 64);
     __shared__ uint8_t symbols[SDR_MAX_SYMS];
@@ -1086,8 +1109,25 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
         return;
     }
     {
-        constexpr int U = 8;                        // loads in flight per lane per round
-        for (int i0 = lane; i0 < n; i0 += 64 * U) {
+        // the whole row in one round of loads where it fits: 16-byte loads when the row is aligned
+        // (VEC4), then the LDS writes
+        constexpr int U4 = 12;
+        int i_tail = 0;
+        if (vec4) {
+            const int n4 = n >> 2;
+            for (int q0 = lane; q0 < n4; q0 += 64 * U4) {
+                float4 v[U4];
+#pragma unroll
+                for (int u = 0; u < U4; u++)
+                    if (q0 + 64 * u < n4) v[u] = reinterpret_cast<const float4*>(xc)[q0 + 64 * u];
+#pragma unroll
+                for (int u = 0; u < U4; u++)
+                    if (q0 + 64 * u < n4) reinterpret_cast<float4*>(xs)[q0 + 64 * u] = v[u];
+            }
+            i_tail = n4 * 4;
+        }
+        constexpr int U = 8;
+        for (int i0 = i_tail + lane; i0 < n; i0 += 64 * U) {
             float v[U];
 #pragma unroll
             for (int u = 0; u < U; u++) v[u] = (i0 + 64 * u < n) ? xc[i0 + 64 * u] : 0.0f;
@@ -1101,44 +1141,39 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
     int m = 0;
     if (off < n) m = (n - off + sps - 1) / sps;     // i with off + i*sps < n
     if (m > SDR_MAX_SYMS) m = SDR_MAX_SYMS;
-    for (int i = lane; i < m; i += blockDim.x) symbols[i] = xs[off + i * sps] > 0;
+    for (int i = lane; i < m; i += 64) symbols[i] = xs[off + i * sps] > 0;
     __syncthreads();
+    // manchester_decode + differential_decode with every lane: bit k of the block is half_symbol
+    // (k < nb0, a symbol pair split across blocks) or symbols[start + 2 (k - nb0)]; the outputs are
+    // bits[k] ^ bits[k-1] (bits[-1] = the previous block's last bit), the state comes from the ends
+    const int half_in = d[1], start_in = d[2], last_in = d[3];
+    const int nb0 = start_in ? 1 : 0;
+    int start = start_in;
+    if (block_count == 0) {  // dead in the reference (decoding starts at block 6), kept for parity
+        int score = 0;
+        for (int i = 0; i < m - 1; i += 2) score += symbols[i] ^ symbols[i + 1];
+        for (int j = 1; j < m - 1; j += 2) score -= symbols[j] ^ symbols[j + 1];
+        start = score < 0;
+    }
+    const int npairs = m - 1 > start ? (m - start) / 2 : 0;       // i = start, start + 2, ... < m - 1
+    const int nb = min(nb0 + npairs, SDR_MAX_BITS);
+    auto bit_at = [&](int k) -> int { return k < nb0 ? half_in : symbols[start + 2 * (k - nb0)]; };
+    uint8_t* bo = bits_out ? bits_out + (size_t)ch * bits_stride : nullptr;
+    if (bo) {
+        for (int k = lane; k < nb; k += 64) {
+            const int prev = k == 0 ? (block_count == 0 ? 0 : last_in) : bit_at(k - 1);
+            bo[k] = (uint8_t)(bit_at(k) ^ prev);
+        }
+    }
+    if (sym_out) {
+        uint8_t* so = sym_out + (size_t)ch * sym_stride;
+        for (int i = lane; i < m; i += 64) so[i] = symbols[i];
+    }
     if (lane == 0) {
-        int half_symbol = d[1], start = d[2], last_bit = d[3];
-        uint8_t bits[SDR_MAX_BITS];
-        int nb = 0;
-        if (start) bits[nb++] = (uint8_t)half_symbol;
-        if (block_count == 0) {  // dead in the reference (decoding starts at block 6), kept for parity
-            int score = 0;
-            for (int i = 0; i < m - 1; i += 2) score += symbols[i] ^ symbols[i + 1];
-            for (int j = 1; j < m - 1; j += 2) score -= symbols[j] ^ symbols[j + 1];
-            start = score < 0;
-        }
-        for (int i = start; i < m - 1 && nb < SDR_MAX_BITS; i += 2) bits[nb++] = symbols[i];
-        if (((m - start) & 0x01) == 1) {
-            half_symbol = symbols[m - 1];
-            start = 1;
-        } else {
-            start = 0;
-        }
-        uint8_t* bo = bits_out ? bits_out + (size_t)ch * bits_stride : nullptr;
-        if (nb > 0) {
-            uint8_t prevb = bits[0];
-            const uint8_t first = (block_count == 0) ? bits[0] : (uint8_t)(bits[0] ^ (uint8_t)last_bit);
-            if (bo) bo[0] = first;
-            for (int i = 1; i < nb; i++) {
-                if (bo) bo[i] = bits[i] ^ prevb;
-                prevb = bits[i];
-            }
-            last_bit = bits[nb - 1];
-        }
-        if (sym_out) {
-            uint8_t* so = sym_out + (size_t)ch * sym_stride;
-            for (int i = 0; i < m; i++) so[i] = symbols[i];
-        }
-        d[1] = half_symbol;
-        d[2] = start;
-        d[3] = last_bit;
+        const bool odd = ((m - start) & 0x01) == 1;
+        d[1] = odd ? symbols[m - 1] : half_in;
+        d[2] = odd ? 1 : 0;
+        d[3] = nb > 0 ? bit_at(nb - 1) : last_in;
         d[4] = off;
         d[0] = block_count + 1;
         if (offset_out) offset_out[ch] = off;
@@ -1500,6 +1535,8 @@ int sdr_hbm_copy(void* dst, const void* src, size_t bytes, void* stream) {
 // Diagnosis builds only (-DSDR_PLL_COUNT=1): the PLL chunk counters; -1 in product builds.
 // Not part of sdr_amd.h.
 extern "C" int sdr_diag_pll_counts(unsigned long long* out, int reset) { return diag_pll_counts(out, reset); }
+// Diagnosis builds only (-DSDR_PLL_WAVES=1): per-wave totals of the last persistent launch; -1 otherwise.
+extern "C" int sdr_diag_pll_waves(unsigned long long* out, int nmax) { return diag_pll_waves(out, nmax); }
 
 int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int flags) {
     if (!out || nch <= 0) return fail(SDR_E_INVALID, "bad arguments");
@@ -1649,6 +1686,7 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     TRY(dalloc(c, &c->st_pll, (size_t)nch));
     TRY(dalloc(c, &c->rds_pll, (size_t)nch));
     TRY(dalloc(c, &c->dec, (size_t)nch * DEC_STATE));
+    TRY(dalloc(c, &c->rel_words, (size_t)2 * sdr_ctx::REL_SLOTS + 1));
     TRY(init_state(c, nullptr));
 #undef TRY
     *out = c;
@@ -1706,6 +1744,40 @@ FrontendArgs frontend_args(const sdr_ctx* c, const uint8_t* iq, size_t iq_stride
     a.fast = (c->flags & SDR_FLAG_FAST_FRONTEND) != 0 && c->fe_afrag != nullptr;
     return a;
 }
+// Parity release across streams (threadsafequeue.h:29-31: a producer reuses a buffer only after its
+// consumers released it). The block of parity p is read by the mono stage, the stereo post stage and
+// the RDS mixer; each stores the count of blocks of that parity it has read into a device word on its
+// stream after its kernels that read them (k_flag_store, ordered after them), and the stages that
+// overwrite parity p two blocks later wait on their stream for the count the host last enqueued
+// (k_flag_wait) -- unless that reader ran on the same stream, whose order already holds. Slots:
+// REL_MONO (fm), REL_STEREO (fm, band, t_st, carrier), REL_RDS (rband, t_rds, ipll). Device words,
+// not HIP events: a cross-stream event wait between the CU-masked streams started the waiting
+// stream 60-200 us after the event's work had completed (profiles/r04/release/), a kernel poll
+// within a few us.
+constexpr unsigned REL_MONO = 1u, REL_STEREO = 2u, REL_RDS = 4u;
+int release_record(sdr_ctx* c, unsigned slot, hipStream_t s) {
+    const int p = c->parity, k = slot == REL_MONO ? 0 : slot == REL_STEREO ? 1 : 2;
+    c->rel_seq[p][k]++;
+    c->rel_stream[p][k] = s;
+    return launch_flag_store(c->rel_words + p * sdr_ctx::REL_SLOTS + k, c->rel_seq[p][k], s);
+}
+int release_wait(sdr_ctx* c, int p, unsigned slots, hipStream_t s) {
+    unsigned mask = 0;
+    for (int k = 0; k < sdr_ctx::REL_SLOTS; k++) {
+        const uint32_t want = c->rel_seq[p][k];
+        if (!(slots & (1u << k)) || want == 0 || c->rel_stream[p][k] == s ||
+            (c->rel_waited_on[p][k] == s && c->rel_waited[p][k] == want))
+            continue;
+        mask |= 1u << k;
+        c->rel_waited[p][k] = want;
+        c->rel_waited_on[p][k] = s;
+    }
+    if (!mask) return SDR_OK;
+    hipLaunchKernelGGL(k_rel_wait, dim3(1), dim3(64), 0, s, c->rel_words + p * sdr_ctx::REL_SLOTS, c->rel_seq[p][0],
+                       c->rel_seq[p][1], c->rel_seq[p][2], mask, c->rel_words + 2 * sdr_ctx::REL_SLOTS);
+    LAUNCH_CHECK();
+    return SDR_OK;
+}
 int check_iq(const sdr_ctx* c, const uint8_t* iq, size_t iq_stride) {
     const sdr_info& in = c->info;
     if (iq_stride < (size_t)2 * in.block_iq || (iq_stride & 1) || (reinterpret_cast<uintptr_t>(iq) & 1))
@@ -1719,6 +1791,8 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     if (!c || !iq) return fail(SDR_E_INVALID, "null argument");
     if (const int r = check_iq(c, iq, iq_stride)) return r;
     const int p = c->parity ^ 1;
+    // fm of parity p (and the pre stages' buffers, so that sdr_pre on this stream has nothing left to wait for)
+    if (const int rw = release_wait(c, p, REL_MONO | REL_STEREO | REL_RDS, S(stream))) return rw;
     const int r = frontend_launch(frontend_args(c, iq, iq_stride, p), S(stream));
     if (r) return r;
     c->parity = p;
@@ -1750,7 +1824,7 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
                                in.n_audio, audio, audio_stride);
         LAUNCH_CHECK();
         c->mono_done = c->block;
-        return SDR_OK;
+        return release_record(c, REL_MONO, S(stream));
     }
     const int tile = 512;
     dim3 grid(cdiv(in.n_audio, tile), c->nch);
@@ -1761,7 +1835,7 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
                        in.audio_upsample, in.audio_decim, in.n_audio, tile, -HIST, (void*)audio, audio_stride);
     LAUNCH_CHECK();
     c->mono_done = c->block;
-    return SDR_OK;
+    return release_record(c, REL_MONO, S(stream));
 }
 
 // The stereo and RDS loop bodies split at their PLL (pre: FIRs feeding the PLL; pll: the serial
@@ -1811,6 +1885,8 @@ int sdr_stereo_pre(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (c->block < 0 || c->st_pre_done == c->block) return fail(SDR_E_INVALID, "stereo_pre: no new block");
     if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "stereo_pre: %d taps", c->ntaps);
+    // band of this parity read by the stereo post stage two blocks back
+    if (const int rw = release_wait(c, c->parity, REL_STEREO, S(stream))) return rw;
     // pilot BPF (stereo.cpp:74) + band BPF (:80) from one staged window of fm_demod
     const int r = fir_rb<2, false>(c, c->fm_cur(), c->fm_stride, c->info.block_if, stereo_fir(c), S(stream));
     if (r) return r;
@@ -1880,7 +1956,7 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
             hipLaunchKernelGGL(k_stereo_out<9>, g, dim3(AT), 0, s, a);
         LAUNCH_CHECK();
         c->stereo_done = c->block;
-        return SDR_OK;
+        return release_record(c, REL_STEREO, s);
     }
     {
         // NCO output of this block's PLL phases (pll.cpp:52), carrier[0] = last of the previous block
@@ -1911,7 +1987,7 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
         LAUNCH_CHECK();
     }
     c->stereo_done = c->block;
-    return SDR_OK;
+    return release_record(c, REL_STEREO, s);
 }
 
 int sdr_stereo(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
@@ -1947,6 +2023,7 @@ int sdr_rds_pre(sdr_ctx* c, void* stream) {
     hipStream_t s = S(stream);
     const int n = c->info.block_if, p = c->parity;
     float* rband = c->rband + p * c->fm_par;
+    if (const int rw = release_wait(c, p, REL_RDS, s)) return rw;   // rband read by the RDS mixer
     // RDS band BPF (rds.cpp:105) into the extended rds_band stream
     hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rband, c->rband + (p ^ 1) * c->fm_par,
                        c->fm_stride, n);
@@ -1987,6 +2064,7 @@ int sdr_pre(sdr_ctx* c, void* stream) {
         return fail(SDR_E_INVALID, "pre: no new block");
     if (!c->rds_on) return sdr_stereo_pre(c, stream);
     if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "pre: %d taps", c->ntaps);
+    if (const int rw = release_wait(c, c->parity, REL_STEREO | REL_RDS, S(stream))) return rw;
     const int r = pre_launch(c, S(stream));
     if (r) return r;
     c->st_pre_done = c->rds_pre_done = c->block;
@@ -2159,6 +2237,7 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
     nparts = std::min(nparts, ntiles);
     const int p = c->parity ^ 1;
     const FrontendArgs a = frontend_args(c, iq, iq_stride, p);
+    if (const int rw = release_wait(c, p, REL_MONO | REL_STEREO | REL_RDS, s)) return rw;
     c->parity = p;                 // the block's buffers (the pre-PLL FIRs read c->parity)
     c->block++;
     // part q: the FIR tiles [x0, x1) and the front-end tiles their windows need (tile j writes
@@ -2173,7 +2252,10 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
         if (fe_end > fe_done) r = frontend_launch(a, s, fe_done, fe_end - fe_done);
         fe_done = std::max(fe_done, fe_end);
         if (!r) r = pre_launch(c, s, x0, x1 - x0);
-        if (!r && q < nparts - 1) r = launch_flag_store(c->pers_words + PLL_WORD_SUB, c->pers_base * PLL_SUB_SCALE + (uint32_t)x1, s);
+        // (capped below PLL_SUB_SCALE: a count above it would reach the values of a later launch)
+        if (!r && q < nparts - 1)
+            r = launch_flag_store(c->pers_words + PLL_WORD_SUB,
+                                  c->pers_base * PLL_SUB_SCALE + std::min((uint32_t)x1, PLL_SUB_SCALE - 1u), s);
         if (r) return r;
     }
     c->st_pre_done = c->rds_pre_done = c->block;
@@ -2299,6 +2381,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         a.n_rds = in.n_rds;
         hipLaunchKernelGGL(k_rds_mix, dim3(cdiv(n + 1, BLK * MIX_R), c->nch), dim3(BLK), 0, s, a);
         LAUNCH_CHECK();
+        if (const int rr = release_record(c, REL_RDS, s)) return rr;   // rband, t_rds, ipll read
     } else {
         {
             PllJobs jobs{};
@@ -2310,6 +2393,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         hipLaunchKernelGGL(k_mix<true>, dim3(cdiv(n, BLK), c->nch), dim3(BLK), 0, s, rband, c->fm_stride,
                            c->pllbuf(c->ipll), c->pll_stride, n, rdc, c->rdc + (p ^ 1) * c->fm_par, c->fm_stride, 50);
         LAUNCH_CHECK();
+        if (const int rr = release_record(c, REL_RDS, s)) return rr;
         hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, s, rfilt, c->rfilt + (p ^ 1) * c->rf_par,
                            c->rf_stride, in.n_rds);
         LAUNCH_CHECK();
@@ -2359,7 +2443,8 @@ int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, s
     hipLaunchKernelGGL(k_rds_bits, dim3(c->nch), dim3(64), 64 * sizeof(int) + (size_t)in.n_rds * sizeof(float),
                        S(stream), c->rds_clean,
                        c->clean_stride, in.n_rds, in.symbol_Fs, c->rds_on, c->dec, offset, nsym, symbols,
-                       sym_stride, nbits, bits, bits_stride, c->post_err());
+                       sym_stride, nbits, bits, bits_stride, c->post_err(),
+                       (reinterpret_cast<uintptr_t>(c->rds_clean) % 16 == 0 && c->clean_stride % 4 == 0) ? 1 : 0);
     LAUNCH_CHECK();
     c->rds_bits_done = c->block;
     return SDR_OK;
@@ -2541,6 +2626,7 @@ int sdr_push_fm_demod(sdr_ctx* c, const float* fm, size_t fm_stride, void* strea
     const sdr_info& in = c->info;
     const int p = c->parity ^ 1;
     float* dst = c->fm + p * c->fm_par;
+    if (const int rw = release_wait(c, p, REL_MONO | REL_STEREO, S(stream))) return rw;
     HIP_TRY(hipMemcpy2DAsync(dst, c->fm_stride * sizeof(float), fm, fm_stride * sizeof(float),
                              in.block_if * sizeof(float), c->nch, hipMemcpyDeviceToDevice, S(stream)));
     hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, S(stream), dst, c->fm + (p ^ 1) * c->fm_par,

@@ -137,6 +137,23 @@ __device__ __forceinline__ void pll_count_chunk(bool ok) {
 }
 #endif
 
+#ifndef SDR_PLL_WAVES
+#define SDR_PLL_WAVES 0   // diagnosis build: per-wave totals of the last persistent launch (sdr_diag_pll_waves)
+#endif
+#if SDR_PLL_WAVES
+// per wave of k_pll_multi: [0] shader cycles inside its blocks, [1] 100 MHz ticks from the start of
+// each block's flag poll to after its acquire, [2] blocks computed, [3] job (0 stereo 19 kHz, 1 RDS
+// 114 kHz) + 1, [4] ticks of [1] until the poll saw the flag, [5] polls that found it unset, [6]
+// blocks whose first poll found it set, [7] ticks between the flag's publication (g_flag_t) and the
+// poll's start, summed over the blocks where it was published first (negative: the wave waited)
+constexpr int PLL_WAVE_SLOTS = 4096, PLL_WAVE_FIELDS = 8;
+__device__ unsigned long long g_pll_waves[PLL_WAVE_SLOTS][PLL_WAVE_FIELDS];
+// the 100 MHz time at which k_flag_store published each block flag value of the launch (indexed by
+// value % 64; g_diag_flag: the launch's block flag word)
+__device__ unsigned long long g_flag_t[64];
+__device__ const uint32_t* g_diag_flag;
+#endif
+
 // TAB: the trigArg offsets come from a table whose range the kernel checked once (pll_run)
 template <bool TAB>
 __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
@@ -604,7 +621,7 @@ __device__ __forceinline__ void gate_wait(InGate& g, int i_end) {
     while (true) {
         const uint32_t f = __hip_atomic_load(g.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t sb = __hip_atomic_load(g.sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int av = (int32_t)(f - g.want) >= 0 ? g.n : (int)min((int32_t)(sb - g.sub_base), 64) * g.tile;
+        int av = (int32_t)(f - g.want) >= 0 ? g.n : (int)min((int32_t)(sb - g.sub_base), (int32_t)PLL_SUB_SCALE - 1) * g.tile;
         av = __builtin_amdgcn_readfirstlane(min(max(av, 0), g.n));
         if (av >= i_end) {
             g.avail = av;
@@ -835,6 +852,10 @@ __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int 
     const bool lane0 = (threadIdx.x & 63) == 0;
     __builtin_amdgcn_s_setprio(3);
     bool dead = false;                                 // uniform across the workgroup
+#if SDR_PLL_WAVES
+    unsigned long long dw_cyc = 0, dw_wait = 0, dw_blocks = 0, dw_spin = 0, dw_polls = 0, dw_ready = 0, dw_early = 0;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) g_diag_flag = pre_flag;
+#endif
     for (int j = 0; j < nblocks; j++) {
         const PllJob& jb = jobs.p[j & 1].j[blockIdx.y];   // p[0]: the parity of the launch's first block
         const uint32_t want = pre_first + (uint32_t)j + 1u;
@@ -846,17 +867,32 @@ __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int 
             // poll with relaxed loads and acquire once: an acquire load at agent scope invalidates
             // the wave's caches (on a multi-XCD device its XCD's L2) on every poll, which slowed the
             // kernels running beside the waiting waves 2-3x
+#if SDR_PLL_WAVES
+            const unsigned long long p0 = dw_polls;
+#endif
             if (threadIdx.x < 64) {
                 while ((int32_t)(__hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0 &&
                        !(parts && (int32_t)(__hip_atomic_load(sub_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
                                             sub_base) >= 1)) {
                     __builtin_amdgcn_s_sleep(4);
+#if SDR_PLL_WAVES
+                    dw_polls++;
+#endif
                     if (__builtin_amdgcn_s_memrealtime() - t0 > PLL_WAIT_TICKS) {
                         dead = true;
                         break;
                     }
                 }
             }
+#if SDR_PLL_WAVES
+            dw_spin += __builtin_amdgcn_s_memrealtime() - t0;
+            dw_ready += dw_polls == p0 ? 1u : 0u;
+            {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                const unsigned long long tf = __hip_atomic_load(&g_flag_t[want & 63], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tf != 0 && tf < t0) dw_early += t0 - tf;
+            }
+#endif
             if (WG > 1) {
                 if (threadIdx.x == 0) sh_dead = dead ? 1 : 0;
                 __syncthreads();
@@ -911,12 +947,30 @@ __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int 
                 // sums over waves: shader cycles and 100 MHz ticks spent on block j (sdr_plls_cycles)
                 __hip_atomic_fetch_add(t_cyc + 2 * j, c1 - c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_fetch_add(t_cyc + 2 * j + 1, r1 - r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if SDR_PLL_WAVES
+                dw_cyc += c1 - c0;
+                dw_wait += r0 - t0;
+                dw_blocks++;
+#endif
             }
             // block sequence pre_first + j done by this wave: its own slot of the ring
             __hip_atomic_fetch_add(done_ring + (pre_first + (uint32_t)j) % PLL_DONE_RING, 1u, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+#if SDR_PLL_WAVES
+    const int slot = ((int)(blockIdx.y * gridDim.x + blockIdx.x)) * WG + (int)(threadIdx.x >> 6);
+    if (lane0 && slot < PLL_WAVE_SLOTS) {
+        g_pll_waves[slot][0] = dw_cyc;
+        g_pll_waves[slot][1] = dw_wait;
+        g_pll_waves[slot][2] = dw_blocks;
+        g_pll_waves[slot][3] = blockIdx.y + 1u;
+        g_pll_waves[slot][4] = dw_spin;
+        g_pll_waves[slot][5] = dw_polls;
+        g_pll_waves[slot][6] = dw_ready;
+        g_pll_waves[slot][7] = dw_early;
+    }
+#endif
 }
 
 // The two ends of the persistent PLLs' hand-offs, as one-wave kernels so that HIP's in-order
@@ -925,6 +979,9 @@ __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int 
 // kernels of the front-end stream; k_flag_wait holds the post stream until the PLL waves have
 // released a block (bounded, like the PLL's own waits).
 __global__ void k_flag_store(uint32_t* flag, uint32_t v) {
+#if SDR_PLL_WAVES
+    if (threadIdx.x == 0 && flag == g_diag_flag) g_flag_t[v & 63] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ void k_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err) {
@@ -1170,6 +1227,24 @@ int diag_pll_counts(unsigned long long* out, int reset) {
 #else
     (void)out;
     (void)reset;
+    return -1;
+#endif
+}
+
+// Diagnosis builds only (-DSDR_PLL_WAVES=1): the per-wave totals of the last persistent launch
+// (g_pll_waves), at most nmax waves of PLL_WAVE_FIELDS (8) values, cleared after the read; -1 in
+// product builds.
+int diag_pll_waves(unsigned long long* out, int nmax) {
+#if SDR_PLL_WAVES
+    const int nw = std::min(nmax, PLL_WAVE_SLOTS);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pll_waves), sizeof(unsigned long long) * PLL_WAVE_FIELDS * nw));
+    static unsigned long long z[PLL_WAVE_SLOTS][PLL_WAVE_FIELDS];
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pll_waves), z, sizeof z));
+    return nw;
+#else
+    (void)out;
+    (void)nmax;
     return -1;
 #endif
 }

@@ -39,7 +39,7 @@ def _kinds(synth):
 
 
 KEYS = ("fm", "mono", "lr", "clean", "offset", "nsym", "symbols", "nbits", "bits")
-SCHEDULES = ("dispatch", "persistent", "persistent_parts")
+SCHEDULES = ("dispatch", "persistent", "persistent_parts", "persistent_release")
 
 
 def _check(args):
@@ -111,7 +111,9 @@ def _run_schedule(torch, pkg, bench, iq, dev, schedule: str) -> dict:
     if persistent:
         pipe.plls_launch(NBLOCKS, stream=s_pll)
     for b in range(NBLOCKS):                               # bench.GpuStepper.step, outputs captured
-        if b >= 2:
+        # persistent_release: no wait of the caller's own -- the library orders the reuse of block
+        # b-2's parity (its mono / stereo post / RDS mixer release counts, sdr_frontend's wait)
+        if b >= 2 and schedule != "persistent_release":
             s_fe.wait_event(post_done[b - 2])
         if parts and b == 0:
             # the pipeline fill: the launch's first block in sample ranges, each published to the PLLs
