@@ -142,7 +142,12 @@ int sdr_rds_dsp(sdr_ctx *ctx, float *rds_clean, size_t rds_stride, void *stream)
  *   rds_pll      114 kHz PLL, x0.5           rds.cpp:119
  *   rds_post     delay, mixer, 247/640, RRC  rds.cpp:122-133
  * Intermediates crossing the split are kept per block parity, so the PLL of block b+1 may run
- * while block b's post part is still running. */
+ * while block b's post part is still running. Parity release (threadsafequeue.h:29-31): the
+ * readers of a block's parity buffers -- sdr_mono, sdr_stereo_post and sdr_rds_post's mixer --
+ * record on their stream that they have read it, and sdr_frontend (likewise sdr_push_fm_demod,
+ * the pre parts and sdr_frontend_pre_parts) waits on its own stream until the readers of block
+ * b-2, which used the same parity, have done so: the caller needs no wait of its own for that
+ * reuse. Outputs handed to the caller (lr, rds_clean, bits) are the caller's to order. */
 int sdr_stereo_pre(sdr_ctx *ctx, void *stream);
 int sdr_stereo_pll(sdr_ctx *ctx, void *stream);
 int sdr_stereo_post(sdr_ctx *ctx, int16_t *lr, size_t lr_stride, void *stream);
