@@ -499,7 +499,9 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
     constexpr int PW = RLC_TN / (BLK / 64);                  // outputs per wave
     const int c0 = blockIdx.y * 64, n0 = blockIdx.x * RLC_TN;
     const int nn = min(RLC_TN, ny - n0);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave index as a scalar: the per-output table reads (ptq, cnt) are then scalar loads issued
+    // together, not vector loads each waiting for every load before it
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int qlo = (ptq[n0] >> 8) - (L - 1);
     const int W = (ptq[n0 + nn - 1] >> 8) - qlo + 1;
     const int SW = W | 1;
@@ -521,15 +523,8 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
                 v[u][k] = (i < W && m >= hist_lo) ? xc[m] : 0.0f;
             }
         }
-#pragma unroll
-        for (int u = 0; u < NR; u++) {
-            const int c = wave + u * (BLK / 64);
-#pragma unroll
-            for (int k = 0; k < RLC_XL; k++) {
-                const int i = lane + 64 * k;
-                if (i < W) sx[c * SW + i] = v[u][k];
-            }
-        }
+        // the polyphase rows' loads go out with the x tile's, before any LDS write waits for them
+        // (one round of global-memory latency per workgroup instead of two)
         float hv[PW][RLC_HL];
 #pragma unroll
         for (int o8 = 0; o8 < PW; o8++) {
@@ -540,6 +535,15 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
             for (int k = 0; k < RLC_HL; k++) {
                 const int j = lane + 64 * k;
                 hv[o8][k] = (j < cn) ? hp[(size_t)ph * L + j] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NR; u++) {
+            const int c = wave + u * (BLK / 64);
+#pragma unroll
+            for (int k = 0; k < RLC_XL; k++) {
+                const int i = lane + 64 * k;
+                if (i < W) sx[c * SW + i] = v[u][k];
             }
         }
 #pragma unroll
@@ -1791,7 +1795,9 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     if (!c || !iq) return fail(SDR_E_INVALID, "null argument");
     if (const int r = check_iq(c, iq, iq_stride)) return r;
     const int p = c->parity ^ 1;
-    // fm of parity p (and the pre stages' buffers, so that sdr_pre on this stream has nothing left to wait for)
+    // fm of parity p, and the pre stages' buffers too (one wait kernel: sdr_pre on this stream then
+    // has nothing left to wait for; waiting for the RDS mixer only before the pre stages measured the
+    // same, profiles/r04/release/)
     if (const int rw = release_wait(c, p, REL_MONO | REL_STEREO | REL_RDS, S(stream))) return rw;
     const int r = frontend_launch(frontend_args(c, iq, iq_stride, p), S(stream));
     if (r) return r;
