@@ -1120,13 +1120,14 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
         if (vec4) {
             const int n4 = n >> 2;
             for (int q0 = lane; q0 < n4; q0 += 64 * U4) {
+                // loads and LDS writes unconditional at a clamped index (lanes past the row rewrite its
+                // last element with the same value): conditional ones went to scratch, or were sunk
+                // next to their writes, one load in flight at a time
                 float4 v[U4];
 #pragma unroll
-                for (int u = 0; u < U4; u++)
-                    if (q0 + 64 * u < n4) v[u] = reinterpret_cast<const float4*>(xc)[q0 + 64 * u];
+                for (int u = 0; u < U4; u++) v[u] = reinterpret_cast<const float4*>(xc)[min(q0 + 64 * u, n4 - 1)];
 #pragma unroll
-                for (int u = 0; u < U4; u++)
-                    if (q0 + 64 * u < n4) reinterpret_cast<float4*>(xs)[q0 + 64 * u] = v[u];
+                for (int u = 0; u < U4; u++) reinterpret_cast<float4*>(xs)[min(q0 + 64 * u, n4 - 1)] = v[u];
             }
             i_tail = n4 * 4;
         }
