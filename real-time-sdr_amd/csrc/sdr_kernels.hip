@@ -1044,8 +1044,7 @@ __global__ void k_demod_prev(float2* __restrict__ prev, const float* __restrict_
 // cdr(), rds_utilities.cpp:4-21: argmax over offsets i < sps of sum_k |(int)x[k*sps+i]|,
 // first maximum wins, 0 when every sum is 0. One wave per channel, one lane per offset; the argmax
 // is a wave reduction of (sum, -offset) over the sums > 0 (the reference's strict > from maxv = 0).
-__device__ __forceinline__ int cdr_wave(const float* x, int n, int sps, int* sums) {
-    (void)sums;
+__device__ __forceinline__ int cdr_wave(const float* x, int n, int sps) {
     const int lane = threadIdx.x;
     const int nk = n / sps;
     unsigned long long key = 0;                     // (sum << 32) | ~offset of this lane's best offset
@@ -1069,9 +1068,8 @@ __device__ __forceinline__ int cdr_wave(const float* x, int n, int sps, int* sum
 
 __global__ __launch_bounds__(64) void k_cdr(int32_t* __restrict__ offset, const float* __restrict__ x,
                                             size_t x_stride, int n, int sps) {
-    extern __shared__ int sums_dyn[];
     const int ch = blockIdx.x;
-    const int off = cdr_wave(x + (size_t)ch * x_stride, n, sps, sums_dyn);
+    const int off = cdr_wave(x + (size_t)ch * x_stride, n, sps);
     if (threadIdx.x == 0) offset[ch] = off;
 }
 
@@ -1084,10 +1082,10 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
                                                  uint8_t* __restrict__ sym_out, size_t sym_stride,
                                                  int32_t* __restrict__ nbits_out, uint8_t* __restrict__ bits_out,
                                                  size_t bits_stride, const uint32_t* __restrict__ err, int vec4) {
-    // dynamic LDS: 64 ints (unused), then the channel's whole block (n floats), staged with every
-    // load in flight (the cdr reads it 39-strided and the slicer sps-strided: from LDS, not global memory)
-    extern __shared__ int sums_dyn[];
-    float* xs = reinterpret_cast<float*>(sums_dyn + 64);
+    // dynamic LDS: the channel's whole block (n floats), staged with every load in flight (the cdr
+    // reads it 39-strided and the slicer sps-strided: from LDS, not global memory)
+    extern __shared__ float4 xs4[];
+    float* xs = reinterpret_cast<float*>(xs4);
     __shared__ uint8_t symbols[SDR_MAX_SYMS];
     const int ch = blockIdx.x;
     const int lane = threadIdx.x;
@@ -1142,7 +1140,7 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
         }
         __syncthreads();
     }
-    const int off = cdr_wave(xs, n, sps, sums_dyn);
+    const int off = cdr_wave(xs, n, sps);
     int m = 0;
     if (off < n) m = (n - off + sps - 1) / sps;     // i with off + i*sps < n
     if (m > SDR_MAX_SYMS) m = SDR_MAX_SYMS;
@@ -2447,7 +2445,7 @@ int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, s
         return fail(SDR_E_INVALID, "rds_bits: run sdr_rds_dsp on a new block first");
     if (const int rf = check_pers_failed(c, "rds_bits")) return rf;
     const sdr_info& in = c->info;
-    hipLaunchKernelGGL(k_rds_bits, dim3(c->nch), dim3(64), 64 * sizeof(int) + (size_t)in.n_rds * sizeof(float),
+    hipLaunchKernelGGL(k_rds_bits, dim3(c->nch), dim3(64), (size_t)in.n_rds * sizeof(float),
                        S(stream), c->rds_clean,
                        c->clean_stride, in.n_rds, in.symbol_Fs, c->rds_on, c->dec, offset, nsym, symbols,
                        sym_stride, nbits, bits, bits_stride, c->post_err(),
@@ -2605,7 +2603,7 @@ int sdr_fmpll(float* out, size_t out_stride, const float* in, size_t in_stride, 
 
 int sdr_cdr(int32_t* offset, const float* x, size_t x_stride, int nch, int n, int sps, void* stream) {
     if (!offset || !x || nch <= 0 || n < 0 || sps <= 0 || sps > 64) return fail(SDR_E_INVALID, "cdr: bad arguments");
-    hipLaunchKernelGGL(k_cdr, dim3(nch), dim3(64), 64 * sizeof(int), S(stream), offset, x, x_stride, n, sps);
+    hipLaunchKernelGGL(k_cdr, dim3(nch), dim3(64), 0, S(stream), offset, x, x_stride, n, sps);
     LAUNCH_CHECK();
     return SDR_OK;
 }
