@@ -42,6 +42,9 @@ def test_diagnosis_counters_absent_in_product_build(pkg):
     the shipped library answers -1 without touching a GPU, and bench.py then reports no redo rate."""
     out = (C.c_ulonglong * 10)()
     assert pkg.lib().sdr_diag_pll_counts(out, 0) == -1
+    # the per-wave totals of -DSDR_PLL_WAVES=1 builds (bench.py pll.waves) likewise
+    waves = (C.c_ulonglong * (8 * 4))()
+    assert pkg.lib().sdr_diag_pll_waves(waves, 4) == -1
 
 
 def test_product_taps_equal_reference_taps(pkg, golden):
