@@ -1040,7 +1040,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 40 untimed blocks (~30 ms): the shader clock settles from ~2316 to ~2380 MHz under the sustained
+    # load only after tens of ms, so a 5-block warm-up times the clock ramp, not the steady state
+    # (profiles/r04/warmup_ab.txt: 20 steps 0.720 ms after 5 warm-up blocks, 0.700-0.702 after 40)
+    ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--channels", type=int, default=1024, help="channels per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL gather (N>1)")
