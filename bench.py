@@ -300,6 +300,9 @@ class GpuStepper:
         # (the RDS chain after its mixer and the output captures are not waited for)
         if b >= 2 and self.fe_waits_post:
             s_fe.wait_event(self.post_done[b - 2])
+        # that wait (a one-wave kernel) goes ahead of the timer, so fe_start..fe_end spans the
+        # front-end kernel alone (the roofline's average launch time; frontend() then waits no more)
+        pipe.release_wait(stream=s_fe)
         self.fe_start[b].record(s_fe)
         if first and self.persist and self.fill_parts > 1:
             # the pipeline fill: the phase's first block in sample ranges, each published to the

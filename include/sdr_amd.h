@@ -29,12 +29,16 @@ extern "C" {
 #define SDR_E_HIP (-2)       /* HIP runtime error (see sdr_last_error) */
 #define SDR_E_NOMEM (-3)
 #define SDR_E_NODEV (-4)     /* no gfx950 device */
+#define SDR_E_TIMEOUT (-5)   /* a parity-release wait gave up (a reader held its block > 5 s): the context's
+                              * outputs are poisoned from then on; every stage call fails until
+                              * sdr_ctx_reset */
 
 #define SDR_MAX_SYMS 256     /* symbols per block, >= n_rds/symbol_Fs + 1 for every mode */
 #define SDR_MAX_BITS 256
 
-/* Outputs of a block whose persistent PLL wait timed out (sdr_plls_launch): the post stages write
- * these instead of audio / bits computed from phases that were never produced. */
+/* Outputs of a block whose persistent PLL wait timed out (sdr_plls_launch), or of any block after a
+ * parity-release wait timed out (SDR_E_TIMEOUT): the output stages write these instead of audio /
+ * bits computed from phases that were never produced or from buffers the producer overwrote. */
 #define SDR_PCM_POISON ((int16_t)-32768)  /* every L/R sample of the block */
 #define SDR_NBITS_POISONED (-2)           /* nbits[ch] of sdr_rds_bits; rds_clean rows are NaN */
 
@@ -121,12 +125,20 @@ int sdr_differential_decode(uint8_t *out, size_t out_stride, const uint8_t *bits
  * (rffrontend.cpp:9-77, mono.cpp:8-50, stereo.cpp:10-115, rds.cpp:11-193) as batched kernels. */
 int sdr_ctx_create(sdr_ctx **out, int device, int nch, int mode, int rds_on, int flags);
 int sdr_ctx_destroy(sdr_ctx *ctx);
-int sdr_ctx_reset(sdr_ctx *ctx, void *stream);      /* all state back to the reference's initial values */
+/* all state back to the reference's initial values; clears a release timeout (SDR_E_TIMEOUT) and the
+ * last persistent launch's hold on the current block. Call it once the streams that ran the context's
+ * stages have drained. */
+int sdr_ctx_reset(sdr_ctx *ctx, void *stream);
 int sdr_ctx_info(const sdr_ctx *ctx, sdr_info *info);
 
 /* RF_frontend loop body (rffrontend.cpp:58-71): iq [nch][2*block_iq] u8 interleaved I/Q ->
  * the context's fm_demod for this block. Advances the context to the next block. */
 int sdr_frontend(sdr_ctx *ctx, const uint8_t *iq, size_t iq_stride, void *stream);
+/* The parity-release wait the next sdr_frontend (or sdr_frontend_pre_parts) begins with, enqueued on
+ * `stream` now (the producer's wait for its consumers' prepare(), threadsafequeue.h:29-31): that call,
+ * on the same stream, then has nothing left to wait for, so a caller can time or order the front-end
+ * kernel alone. Optional. */
+int sdr_frontend_release_wait(sdr_ctx *ctx, void *stream);
 /* mono loop body (mono.cpp:34-42) on the current block: audio [nch][n_audio] int16 */
 int sdr_mono(sdr_ctx *ctx, int16_t *audio, size_t audio_stride, void *stream);
 /* stereo loop body (stereo.cpp:74-107): lr [nch][2*n_audio] int16, L/R interleaved */
@@ -147,7 +159,11 @@ int sdr_rds_dsp(sdr_ctx *ctx, float *rds_clean, size_t rds_stride, void *stream)
  * record on their stream that they have read it, and sdr_frontend (likewise sdr_push_fm_demod,
  * the pre parts and sdr_frontend_pre_parts) waits on its own stream until the readers of block
  * b-2, which used the same parity, have done so: the caller needs no wait of its own for that
- * reuse. Outputs handed to the caller (lr, rds_clean, bits) are the caller's to order. */
+ * reuse. Outputs handed to the caller (lr, rds_clean, bits) are the caller's to order. The wait is
+ * bounded (5 s): a reader that has not released its block by then makes it an error, never wrong
+ * output -- the producer goes on, every output stage that runs afterwards writes SDR_PCM_POISON
+ * audio (mono and stereo), NaN rds_clean rows and nbits = SDR_NBITS_POISONED, and every later call
+ * on the context returns SDR_E_TIMEOUT until sdr_ctx_reset. */
 int sdr_stereo_pre(sdr_ctx *ctx, void *stream);
 int sdr_stereo_pll(sdr_ctx *ctx, void *stream);
 int sdr_stereo_post(sdr_ctx *ctx, int16_t *lr, size_t lr_stride, void *stream);

@@ -24,9 +24,10 @@ HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ["SDR_AMD_LIB"]) if os.environ.get("SDR_AMD_LIB") else HERE / "libsdr_amd.so"  # override: A/B experiments (tools/)
 
 SDR_OK = 0
+SDR_E_TIMEOUT = -5           # a parity-release wait gave up: outputs poisoned until reset (include/sdr_amd.h)
 SDR_MAX_SYMS = 256
 SDR_MAX_BITS = 256
-SDR_PCM_POISON = -32768      # audio of a block whose persistent PLL wait timed out (include/sdr_amd.h)
+SDR_PCM_POISON = -32768      # audio of a block whose persistent PLL or release wait timed out (include/sdr_amd.h)
 SDR_NBITS_POISONED = -2      # nbits of such a block (its rds_clean rows are NaN)
 FLAG_FAST_FRONTEND = 0x1
 FLAG_PLL_LIBM = 0x2
@@ -36,7 +37,9 @@ _lib = None
 
 
 class SdrError(RuntimeError):
-    pass
+    def __init__(self, msg: str, code: int | None = None):
+        super().__init__(msg)
+        self.code = code
 
 
 class PllState(C.Structure):
@@ -78,6 +81,7 @@ def lib() -> C.CDLL:
         "sdr_ctx_reset": ([vp, vp], i32),
         "sdr_ctx_info": ([vp, C.POINTER(Info)], i32),
         "sdr_frontend": ([vp, vp, sz, vp], i32),
+        "sdr_frontend_release_wait": ([vp, vp], i32),
         "sdr_mono": ([vp, vp, sz, vp], i32),
         "sdr_stereo": ([vp, vp, sz, vp], i32),
         "sdr_rds_dsp": ([vp, vp, sz, vp], i32),
@@ -114,7 +118,7 @@ def lib() -> C.CDLL:
 def check(rc: int, what: str = "") -> None:
     if rc != SDR_OK:
         msg = lib().sdr_last_error().decode(errors="replace")
-        raise SdrError(f"{what} failed ({rc}): {msg}")
+        raise SdrError(f"{what} failed ({rc}): {msg}", rc)
 
 
 def hbm_copy(dst, src, stream=None) -> None:
@@ -280,6 +284,11 @@ class Pipeline:
     def frontend(self, iq, stream=None):
         """iq: uint8 [nch][2*block_iq] (device)."""
         check(lib().sdr_frontend(self._h, _ptr(iq), _row_stride(iq), _stream(stream)), "sdr_frontend")
+
+    def release_wait(self, stream=None):
+        """The parity-release wait of the next frontend(), enqueued now on `stream` (that call then
+        enqueues none there): the front-end kernel can be timed alone."""
+        check(lib().sdr_frontend_release_wait(self._h, _stream(stream)), "sdr_frontend_release_wait")
 
     def fm_demod(self, out=None, stream=None):
         import torch

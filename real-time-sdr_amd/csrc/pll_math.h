@@ -315,18 +315,16 @@ PLLM_HD SinCosR sincos_r(float t) {
 // v3 step pieces (k_pll): fewer instructions per step, same values.
 //  * sincos_rn: the reduction rounds -t (2/pi) against MAGIC + 1, so the low word of the rounded
 //    value is nq1 = 1 - q (mod 2^32) -- exactly what base_angle needs -- and kdn = -kd folds its
-//    sign into the two reduction fmas. PLL_POLY = 1 evaluates both kernels by Horner (2
-//    multiplies fewer than Estrin's z^2, z^4 powers, a longer dependent chain) with the refitted
-//    5-coefficient sin (SR1..SR5, one fma fewer than fdlibm's), 0 by Estrin with fdlibm's sin.
+//    sign into the two reduction fmas. Both kernels by Horner (2 multiplies fewer than Estrin's
+//    z^2, z^4 powers, a longer dependent chain: +1.8 %; a two-level form, +3.4 %, is
+//    tools/patches/pll_variants.patch) with the refitted 5-coefficient sin (SR1..SR5, one fma fewer
+//    than fdlibm's).
 //  * base_angle_n(nlo, nq1, b, mr) = base_angle(nlo, 1 - nq1, b, mr): one 3-input add.
 // ------------------------------------------------------------------------------------------
-#ifndef PLL_POLY
-#define PLL_POLY 1
-#endif
 constexpr double MAGIC1 = 6755399441055745.0;   // 1.5 * 2^52 + 1
 
 struct SinCosRN {
-    double cr, sr;   // cos r, sin r (relative error < 2^-51.7, 2^-47.4 with PLL_POLY 1)
+    double cr, sr;   // cos r, sin r (relative error < 2^-51.7, 2^-47.4)
     double r;        // t - q pi/2 in [-pi/4, pi/4]
     uint32_t nq1;    // 1 - q (mod 2^32)
     uint32_t b;      // [r < 0]
@@ -336,16 +334,6 @@ struct SinCosRN {
 
 PLLM_HD void sincos_kernels(double r, double& cr, double& sr) {
     const double z = r * r;
-#if PLL_POLY == 2
-    // two-level: P = (a0 + z a1) + z^2 ((a2 + z a3) + z^2 a4) -- one multiply (z^2) more than
-    // Horner, 4 dependent operations after z instead of 6 (cos) / 5 (sin); 2^-47.48 (sin),
-    // 2^-51.79 (cos) relative in double evaluation
-    const double z2 = z * z;
-    const double sp = fma_(z2, fma_(z2, SR5, fma_(z, SR4, SR3)), fma_(z, SR2, SR1));
-    const double cq = fma_(z2, fma_(z2, C5, fma_(z, C4, C3)), fma_(z, C2, C1));
-    sr = fma_(r * z, sp, r);
-    cr = fma_(z2, cq, fma_(z, -0.5, 1.0));
-#elif PLL_POLY
     double sp = fma_(z, SR5, SR4);
     sp = fma_(z, sp, SR3);
     sp = fma_(z, sp, SR2);
@@ -357,14 +345,6 @@ PLLM_HD void sincos_kernels(double r, double& cr, double& sr) {
     cp = fma_(z, cp, -0.5);
     sr = fma_(r * z, sp, r);
     cr = fma_(z, cp, 1.0);
-#else
-    const double z2 = z * z;
-    const double z4 = z2 * z2;
-    const double sp = fma_(z4, fma_(z, S6, S5), fma_(z2, fma_(z, S4, S3), fma_(z, S2, S1)));
-    const double cp = fma_(z4, C5, fma_(z2, fma_(z, C4, C3), fma_(z, C2, C1)));
-    sr = fma_(r * z, sp, r);
-    cr = fma_(z2, cp, fma_(z, -0.5, 1.0));
-#endif
 }
 
 // valid for |t| < T_MAX (the caller checks the range)

@@ -204,15 +204,29 @@ struct sdr_ctx {
     // 2 sdr_rds_post's mixer (rband, t_rds, ipll), stored on the reader's stream (rel_stream) after
     // its kernels; the producers of the block two later wait for the count on their own streams
     static constexpr int REL_SLOTS = 3;
-    uint32_t* rel_words = nullptr;                      // [2][REL_SLOTS] counters + 1 timeout word
+    uint32_t* rel_words = nullptr;                      // [2][REL_SLOTS] counters
     uint32_t rel_seq[2][REL_SLOTS] = {};
     hipStream_t rel_stream[2][REL_SLOTS] = {};
     uint32_t rel_waited[2][REL_SLOTS] = {};            // the count a wait on rel_waited_on already covers
     hipStream_t rel_waited_on[2][REL_SLOTS] = {};
     bool pers_failed = false;                           // sdr_plls_report saw a timeout of the current launch
-    // the error word the post stages of the current block check (their outputs are poisoned when a
-    // persistent wait timed out): only for blocks signalled through a persistent launch
-    const uint32_t* post_err() const { return (pers_words && pers_block == block) ? pers_words + 1 : nullptr; }
+    // streams whose post stages read the last launch's error word (sdr_plls_wait): the next launch's
+    // prepare clears that word only after them (events recorded on each, waited for on its stream)
+    static constexpr int PERS_READERS = 4;
+    hipStream_t pers_readers[PERS_READERS] = {};
+    int pers_nreaders = 0;
+    hipEvent_t pers_reader_ev[PERS_READERS] = {};
+    // the persistent launch's error word the post stages of the current block check (their outputs
+    // are poisoned when a persistent wait timed out): only for blocks signalled through a launch
+    const uint32_t* pers_err() const { return (pers_words && pers_block == block) ? pers_words + 1 : nullptr; }
+    // release timeout (sdr_kernels.hip release_wait): fail_words[0] is set on the device by a parity
+    // release wait that gave up (a reader had not released a buffer within ~5 s, and the producer
+    // then overwrote it); every output stage poisons its block while it is set, and the same wait sets
+    // the host-mapped *fail_host, which every later stage call checks (SDR_E_TIMEOUT). sdr_ctx_reset
+    // clears both.
+    uint32_t* fail_words = nullptr;
+    uint32_t* fail_host = nullptr;                      // hipHostMalloc'd (coherent), host view
+    uint32_t* fail_host_dev = nullptr;                  // its device address
     std::vector<void*> allocs;
 
     float* fm_cur() const { return fm + parity * fm_par; }

@@ -67,6 +67,24 @@ __device__ __forceinline__ int16_t cvt_i16_x86(float v) {
     return (int16_t)(uint16_t)((uint32_t)cvt_i32_x86(v) & 0xFFFFu);
 }
 
+// The error words an output stage checks before it hands out a block (SDR_PCM_POISON audio, NaN
+// rds_clean rows, nbits = SDR_NBITS_POISONED instead of outputs, include/sdr_amd.h):
+//   pers  the persistent PLL launch that produced this block's phases (null for other blocks)
+//   fail  the context's sticky release-timeout word: a producer overwrote a parity buffer whose
+//         readers had not released it within the bounded wait (release_wait), so any reader that
+//         runs after it may read the next block's data; set until sdr_ctx_reset.
+struct Poison {
+    const uint32_t* pers;
+    const uint32_t* fail;
+};
+// read once per wave (scalar loads of kernel-argument addresses; the value is made wave-uniform)
+__device__ __forceinline__ uint32_t poison_word(const Poison& p) {
+    uint32_t v = 0;
+    if (p.pers) v |= *p.pers;
+    if (p.fail) v |= *p.fail;
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
 // ------------------------------------------------------------------------------------------
 // Decimating FIR, filter.cpp:106-121: y[n] = sum_{k<ntaps} h[k] * x[nD-k], ascending k, f32
 // mul then add. x[m] for m < 0 comes from `hist` (hist[m], m >= -nhist). NT = 1 or 2 tap sets
@@ -144,8 +162,8 @@ struct FirRb {
     double* rx0;
     size_t rx_stride;
     const float* hist2_src;
-    const uint32_t* err;       // non-null: poison the outputs (NaN) when *err != 0 (a persistent PLL timeout)
-    float* ydup;               // non-null: y[0] stored here too (stride ydup_stride)
+    Poison err;                // {null, null}, or the block's error words: NaN outputs when one is set
+    float* ydup;              // non-null: y[0] stored here too (stride ydup_stride)
     size_t ydup_stride;
     int x0;                    // first tile (blockIdx.x + x0): a part of the block (sdr_frontend_pre_parts)
 };
@@ -160,7 +178,10 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
     static_assert(!PK || NT == 3, "packed pairs: sets 0 and 1 of a 3-set pass");
     constexpr int T = FRB_T, R = FRB_R;
     __shared__ __attribute__((aligned(16))) float sx[(FRB_W + 3) & ~3];
+    __shared__ uint32_t s_poison;                                 // one decision per workgroup
     const int ch = blockIdx.y, tid = threadIdx.x;
+    const bool checks = f.err.pers || f.err.fail;
+    if (checks && tid == 0) s_poison = poison_word(f.err);        // (its latency hides behind the staging)
     const int xt = (int)blockIdx.x + f.x0;                        // tile of the block
     const int n0 = xt * FRB_TILE;
     const int m0 = n0 - (T - 1);
@@ -306,7 +327,7 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
     for (int t = 0; t < NT; t++)
 #pragma unroll
         for (int j = 0; j < R; j++) asm volatile("" : "+v"(a[t][j]));
-    if (f.err && *f.err != 0u) {                                  // no valid input behind this block
+    if (checks && s_poison != 0u) {                               // no valid input behind this block
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
@@ -716,10 +737,13 @@ constexpr int audio_tw() { return (D * (AR - 1) + 101 + 3) / 4 * 4; }   // windo
 template <int D>
 __global__ __launch_bounds__(AT) void k_mono_out(const float* __restrict__ fm, size_t fm_stride,
                                                  const float* __restrict__ h, int n, int ny,
-                                                 int16_t* __restrict__ audio, size_t audio_stride) {
+                                                 int16_t* __restrict__ audio, size_t audio_stride,
+                                                 const Poison err) {
     constexpr int WIN = audio_win<D>(), TW = audio_tw<D>();
     __shared__ __attribute__((aligned(16))) float sa[(WIN + 3) / 4 * 4 + 4];
+    __shared__ uint32_t s_poison;                            // one decision per workgroup
     const int ch = blockIdx.y, tid = threadIdx.x;
+    if (tid == 0) s_poison = poison_word(err);
     const int o0 = blockIdx.x * ATILE;
     const int m0 = D * o0 - 100;
     const float* x = fm + (size_t)ch * fm_stride;
@@ -739,10 +763,16 @@ __global__ __launch_bounds__(AT) void k_mono_out(const float* __restrict__ fm, s
     __syncthreads();
     const int ob = o0 + tid * AR;
     if (ob >= ny) return;
+    int16_t* o = audio + (size_t)ch * audio_stride + ob;
+    if (s_poison != 0u) {        // fm_demod may hold another block's samples (a release wait timed out)
+#pragma unroll
+        for (int r = 0; r < AR; r++)
+            if (ob + r < ny) o[r] = SDR_PCM_POISON;
+        return;
+    }
     float w[TW], acc[AR];
     audio_window<D>(sa, tid, w);
     audio_mac<D>(h, w, acc);
-    int16_t* o = audio + (size_t)ch * audio_stride + ob;
 #pragma unroll
     for (int r = 0; r < AR; r++)
         if (ob + r < ny) o[r] = cvt_i16_x86(16384 * acc[r]);   // mono.cpp:41
@@ -775,7 +805,7 @@ struct StereoOut {
     int n, ny;
     int16_t* lr;
     size_t lr_stride;
-    const uint32_t* err;        // non-null: a persistent PLL launch produced the phases (its error word)
+    Poison err;                 // the block's error words (persistent PLL launch, release timeout)
 };
 
 template <int D>
@@ -783,19 +813,10 @@ __global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
     constexpr int WIN = audio_win<D>(), TW = audio_tw<D>();
     __shared__ __attribute__((aligned(16))) float sa[(WIN + 3) / 4 * 4 + 4];
     __shared__ __attribute__((aligned(16))) float sb[(WIN + 3) / 4 * 4 + 4];
+    __shared__ uint32_t s_poison;                                  // one decision per workgroup
     const int ch = blockIdx.y, tid = threadIdx.x;
     const int o0 = blockIdx.x * ATILE;
-    if (a.err && *a.err != 0u) {
-        // a persistent PLL wait timed out: this block's phases were never computed (or not yet),
-        // so the consumer gets a marked block instead of audio (include/sdr_amd.h SDR_PCM_POISON)
-        const int ob = o0 + tid * AR;
-        uint32_t* o = reinterpret_cast<uint32_t*>(a.lr + (size_t)ch * a.lr_stride) + ob;
-        const uint32_t pp = (uint32_t)(uint16_t)SDR_PCM_POISON * 0x10001u;
-#pragma unroll
-        for (int r = 0; r < AR; r++)
-            if (ob + r < a.ny) o[r] = pp;
-        return;
-    }
+    if (tid == 0) s_poison = poison_word(a.err);                   // read beside the staging loads
     const int m0 = D * o0 - 100;
     const bool last_tile = o0 + ATILE >= a.ny;
     // the last tile also computes up to the block end: stereo_dc's tail is the next block's history
@@ -839,12 +860,22 @@ __global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
     __syncthreads();
     const int ob = o0 + tid * AR;
     if (ob >= a.ny) return;
+    uint32_t* o = reinterpret_cast<uint32_t*>(a.lr + (size_t)ch * a.lr_stride) + ob;
+    if (s_poison != 0u) {
+        // a persistent PLL wait timed out (this block's phases were never computed, or not yet) or a
+        // release wait did (the inputs may hold another block): the consumer gets a marked block
+        // instead of audio (include/sdr_amd.h SDR_PCM_POISON)
+        const uint32_t pp = (uint32_t)(uint16_t)SDR_PCM_POISON * 0x10001u;
+#pragma unroll
+        for (int r = 0; r < AR; r++)
+            if (ob + r < a.ny) o[r] = pp;
+        return;
+    }
     float w[TW], m[AR], sv[AR];
     audio_window<D>(sa, tid, w);
     audio_mac<D>(a.h, w, m);                                       // mono resampler (:94)
     audio_window<D>(sb, tid, w);
     audio_mac<D>(a.h, w, sv);                                      // stereo resampler (:97)
-    uint32_t* o = reinterpret_cast<uint32_t*>(a.lr + (size_t)ch * a.lr_stride) + ob;
 #pragma unroll
     for (int r = 0; r < AR; r++) {
         if (ob + r < a.ny) {
@@ -855,11 +886,11 @@ __global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
     }
 }
 
-// the unfused stereo post stage's poison (SDR_FLAG_KEEP_INTERMEDIATES): rows [nch][n] of int16
-// overwritten with SDR_PCM_POISON when a persistent PLL wait timed out
-__global__ __launch_bounds__(BLK) void k_poison_i16(const uint32_t* __restrict__ err, int16_t* __restrict__ p,
-                                                    size_t stride, int n) {
-    if (*err == 0u) return;
+// the unfused post stages' poison (SDR_FLAG_KEEP_INTERMEDIATES, the generic resamplers): rows
+// [nch][n] of int16 overwritten with SDR_PCM_POISON when one of the block's error words is set
+__global__ __launch_bounds__(BLK) void k_poison_i16(const Poison err, int16_t* __restrict__ p, size_t stride,
+                                                    int n) {
+    if (poison_word(err) == 0u) return;
     const int i = blockIdx.x * BLK + threadIdx.x;
     if (i < n) p[(size_t)blockIdx.y * stride + i] = SDR_PCM_POISON;
 }
@@ -966,21 +997,30 @@ __global__ __launch_bounds__(BLK) void k_mix(const float* __restrict__ a, size_t
 
 // The parity-release wait (release_wait): every word w[k] with bit k of mask reaches want[k] (counts
 // stored by k_flag_store after the readers' kernels); polled relaxed, acquired once, bounded like the
-// persistent PLL's waits (after ~5 s the wait records 1 in *err and lets the stream go on)
+// persistent PLL's waits. After ~5 s it gives up: it sets the context's sticky fail word (every output
+// stage then poisons its block: a reader that runs after the producer's overwrite would read the
+// next block's data) and its host-mapped mirror (the next stage call returns SDR_E_TIMEOUT) before it
+// lets the stream go on, so no reader can start after the overwrite without seeing the word.
 __global__ void k_rel_wait(const uint32_t* w, uint32_t want0, uint32_t want1, uint32_t want2, unsigned mask,
-                           uint32_t* err) {
+                           uint32_t* fail, uint32_t* fail_host) {
     if (threadIdx.x != 0) return;
     const uint32_t want[3] = {want0, want1, want2};
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (int k = 0; k < 3; k++) {
+    bool expired = false;
+    for (int k = 0; k < 3 && !expired; k++) {
         if (!(mask & (1u << k))) continue;
         while ((int32_t)(__hip_atomic_load(w + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want[k]) < 0) {
             __builtin_amdgcn_s_sleep(4);
             if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {
-                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                expired = true;
                 break;
             }
         }
+    }
+    if (expired) {
+        __hip_atomic_fetch_or(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fail_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");          // both visible before the kernel ends
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
@@ -1081,7 +1121,7 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
                                                  int32_t* __restrict__ offset_out, int32_t* __restrict__ nsym_out,
                                                  uint8_t* __restrict__ sym_out, size_t sym_stride,
                                                  int32_t* __restrict__ nbits_out, uint8_t* __restrict__ bits_out,
-                                                 size_t bits_stride, const uint32_t* __restrict__ err, int vec4) {
+                                                 size_t bits_stride, const Poison err, int vec4) {
     // dynamic LDS: the channel's whole block (n floats), staged with every load in flight (the cdr
     // reads it 39-strided and the slicer sps-strided: from LDS, not global memory)
     extern __shared__ float4 xs4[];
@@ -1093,7 +1133,7 @@ __global__ __launch_bounds__(64) void k_rds_bits(const float* __restrict__ x, si
     const int block_count = d[0];
     const float* xc = x + (size_t)ch * x_stride;
     const bool decode = (block_count > 5) && rds_on;
-    if (err && *err != 0u) {   // a persistent PLL wait timed out: no bits from this block
+    if (poison_word(err) != 0u) {   // a persistent PLL or release wait timed out: no bits from this block
         if (lane == 0) {
             if (offset_out) offset_out[ch] = -1;
             if (nsym_out) nsym_out[ch] = 0;
@@ -1535,6 +1575,21 @@ int sdr_hbm_copy(void* dst, const void* src, size_t bytes, void* stream) {
     return SDR_OK;
 }
 
+// Test support (not part of sdr_amd.h): hold `stream` for `ms` milliseconds (at most 10 s) with one
+// sleeping wave, so that a test can keep a reader stream from releasing its block (the bounded
+// release wait's timeout, tests/test_gpu_pipeline.py).
+__global__ void k_hold(unsigned long long ticks) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+extern "C" int sdr_diag_hold(void* stream, int ms) {
+    if (ms < 0 || ms > 10000) return fail(SDR_E_INVALID, "sdr_diag_hold: %d ms outside [0, 10000]", ms);
+    hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, S(stream), (unsigned long long)ms * 100000ull);
+    HIP_TRY(hipGetLastError());
+    return SDR_OK;
+}
+
 // Diagnosis builds only (-DSDR_PLL_COUNT=1): the PLL chunk counters; -1 in product builds.
 // Not part of sdr_amd.h.
 extern "C" int sdr_diag_pll_counts(unsigned long long* out, int reset) { return diag_pll_counts(out, reset); }
@@ -1689,7 +1744,21 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
     TRY(dalloc(c, &c->st_pll, (size_t)nch));
     TRY(dalloc(c, &c->rds_pll, (size_t)nch));
     TRY(dalloc(c, &c->dec, (size_t)nch * DEC_STATE));
-    TRY(dalloc(c, &c->rel_words, (size_t)2 * sdr_ctx::REL_SLOTS + 1));
+    TRY(dalloc(c, &c->rel_words, (size_t)2 * sdr_ctx::REL_SLOTS));
+    TRY(dalloc(c, &c->fail_words, (size_t)2));
+    {
+        // the release timeout's host-visible mirror: one coherent host word the device sets only on
+        // the failure path, so that every stage call can check it without a synchronisation
+        void* hp = nullptr;
+        if (hipHostMalloc(&hp, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess || !hp)
+            TRY(fail(SDR_E_NOMEM, "hipHostMalloc of the context's fail word"));
+        c->fail_host = static_cast<uint32_t*>(hp);
+        *c->fail_host = 0u;
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess || !dp)
+            TRY(fail(SDR_E_HIP, "hipHostGetDevicePointer of the context's fail word"));
+        c->fail_host_dev = static_cast<uint32_t*>(dp);
+    }
     TRY(init_state(c, nullptr));
 #undef TRY
     *out = c;
@@ -1700,7 +1769,10 @@ int sdr_ctx_destroy(sdr_ctx* c) {
     if (!c) return SDR_OK;
     (void)hipSetDevice(c->device);
     for (void* p : c->allocs) (void)hipFree(p);
+    if (c->fail_host) (void)hipHostFree(c->fail_host);
     if (c->pers_ev) (void)hipEventDestroy(c->pers_ev);
+    for (hipEvent_t e : c->pers_reader_ev)
+        if (e) (void)hipEventDestroy(e);
     delete c;
     return SDR_OK;
 }
@@ -1709,7 +1781,19 @@ int sdr_ctx_reset(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     HIP_TRY(hipSetDevice(c->device));
     c->pers_failed = false;   // a timed-out launch's poisoned state is what the reset replaces
-    return init_state(c, S(stream));
+    // no block of the reset context belongs to the last launch any more (its error word stays set
+    // until the next launch's prepare: a block with the old index must not read it)
+    c->pers_block = -1;
+    c->pers_nreaders = 0;     // (the caller has drained its streams: nothing left to order after)
+    // the release words back in step with the host's counts (a reader that never ran would leave its
+    // slot short, and every later wait on it would expire again), then the release timeout cleared:
+    // callers reset once the streams that ran the context's stages have drained
+    hipStream_t s = S(stream);
+    HIP_TRY(hipMemcpyAsync(c->rel_words, c->rel_seq, sizeof(c->rel_seq), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(c->fail_words, 0, 2 * sizeof(uint32_t), s));
+    const int r = init_state(c, s);   // (synchronises s)
+    __atomic_store_n(c->fail_host, 0u, __ATOMIC_SEQ_CST);
+    return r;
 }
 
 int sdr_ctx_info(const sdr_ctx* c, sdr_info* info) {
@@ -1777,10 +1861,21 @@ int release_wait(sdr_ctx* c, int p, unsigned slots, hipStream_t s) {
     }
     if (!mask) return SDR_OK;
     hipLaunchKernelGGL(k_rel_wait, dim3(1), dim3(64), 0, s, c->rel_words + p * sdr_ctx::REL_SLOTS, c->rel_seq[p][0],
-                       c->rel_seq[p][1], c->rel_seq[p][2], mask, c->rel_words + 2 * sdr_ctx::REL_SLOTS);
+                       c->rel_seq[p][1], c->rel_seq[p][2], mask, c->fail_words, c->fail_host_dev);
     LAUNCH_CHECK();
     return SDR_OK;
 }
+// a parity-release wait of this context gave up (k_rel_wait set the host-mapped fail word): every
+// stage call fails until sdr_ctx_reset (the device poisons the outputs of the stages already queued)
+int check_failed(const sdr_ctx* c, const char* what) {
+    if (c->fail_host && __atomic_load_n(c->fail_host, __ATOMIC_ACQUIRE) != 0u)
+        return fail(SDR_E_TIMEOUT, "%s: a parity-release wait timed out (a reader did not release its block within "
+                                   "5 s, and the producer overwrote it): outputs since are poisoned; sdr_ctx_reset",
+                    what);
+    return SDR_OK;
+}
+// the error words of the current block's output stages (kernel side: Poison)
+Poison block_poison(const sdr_ctx* c) { return Poison{c->pers_err(), c->fail_words}; }
 int check_iq(const sdr_ctx* c, const uint8_t* iq, size_t iq_stride) {
     const sdr_info& in = c->info;
     if (iq_stride < (size_t)2 * in.block_iq || (iq_stride & 1) || (reinterpret_cast<uintptr_t>(iq) & 1))
@@ -1792,6 +1887,7 @@ int check_iq(const sdr_ctx* c, const uint8_t* iq, size_t iq_stride) {
 
 int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) {
     if (!c || !iq) return fail(SDR_E_INVALID, "null argument");
+    if (const int rf_ = check_failed(c, "frontend")) return rf_;
     if (const int r = check_iq(c, iq, iq_stride)) return r;
     const int p = c->parity ^ 1;
     // fm of parity p, and the pre stages' buffers too (one wait kernel: sdr_pre on this stream then
@@ -1805,8 +1901,17 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     return SDR_OK;
 }
 
+int sdr_frontend_release_wait(sdr_ctx* c, void* stream) {
+    if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "frontend_release_wait")) return rf_;
+    // the wait the next sdr_frontend (or sdr_frontend_pre_parts) enqueues first; it then finds the
+    // counts already waited for on this stream and enqueues none
+    return release_wait(c, c->parity ^ 1, REL_MONO | REL_STEREO | REL_RDS, S(stream));
+}
+
 int sdr_get_fm_demod(sdr_ctx* c, float* fm, size_t fm_stride, void* stream) {
     if (!c || !fm) return fail(SDR_E_INVALID, "null argument");
+    if (const int rf_ = check_failed(c, "get_fm_demod")) return rf_;
     if (c->block < 0) return fail(SDR_E_INVALID, "no block processed yet");
     const sdr_info& in = c->info;
     HIP_TRY(hipMemcpy2DAsync(fm, fm_stride * sizeof(float), c->fm_cur(), c->fm_stride * sizeof(float),
@@ -1816,6 +1921,7 @@ int sdr_get_fm_demod(sdr_ctx* c, float* fm, size_t fm_stride, void* stream) {
 
 int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
     if (!c || !audio) return fail(SDR_E_INVALID, "null argument");
+    if (const int rf_ = check_failed(c, "mono")) return rf_;
     if (c->block < 0 || c->mono_done == c->block) return fail(SDR_E_INVALID, "mono: no new block");
     const sdr_info& in = c->info;
     const float* fm = c->fm_cur();
@@ -1823,10 +1929,10 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
         const dim3 g(cdiv(in.n_audio, ATILE), c->nch);
         if (in.audio_decim == 5)
             hipLaunchKernelGGL(k_mono_out<5>, g, dim3(AT), 0, S(stream), fm, c->fm_stride, c->audio_pp, in.block_if,
-                               in.n_audio, audio, audio_stride);
+                               in.n_audio, audio, audio_stride, block_poison(c));
         else
             hipLaunchKernelGGL(k_mono_out<9>, g, dim3(AT), 0, S(stream), fm, c->fm_stride, c->audio_pp, in.block_if,
-                               in.n_audio, audio, audio_stride);
+                               in.n_audio, audio, audio_stride, block_poison(c));
         LAUNCH_CHECK();
         c->mono_done = c->block;
         return release_record(c, REL_MONO, S(stream));
@@ -1838,6 +1944,9 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
     hipLaunchKernelGGL(km, grid, dim3(BLK), lds, S(stream), fm, fm, c->fm_stride, c->fm_stride,
                        nullptr, nullptr, (size_t)0, (size_t)0, c->audio_pp, c->audio_cnt, c->audio_L,
                        in.audio_upsample, in.audio_decim, in.n_audio, tile, -HIST, (void*)audio, audio_stride);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_poison_i16, dim3(cdiv(in.n_audio, BLK), c->nch), dim3(BLK), 0, S(stream), block_poison(c),
+                       audio, audio_stride, in.n_audio);
     LAUNCH_CHECK();
     c->mono_done = c->block;
     return release_record(c, REL_MONO, S(stream));
@@ -1888,6 +1997,7 @@ FirRb stereo_fir(sdr_ctx* c) {
 
 int sdr_stereo_pre(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "stereo_pre")) return rf_;
     if (c->block < 0 || c->st_pre_done == c->block) return fail(SDR_E_INVALID, "stereo_pre: no new block");
     if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "stereo_pre: %d taps", c->ntaps);
     // band of this parity read by the stereo post stage two blocks back
@@ -1901,6 +2011,7 @@ int sdr_stereo_pre(sdr_ctx* c, void* stream) {
 
 int sdr_stereo_pll(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "stereo_pll")) return rf_;
     if (c->st_pre_done != c->block || c->st_pll_done == c->block)
         return fail(SDR_E_INVALID, "stereo_pll: run sdr_stereo_pre on a new block first");
     PllJobs jobs{};
@@ -1914,7 +2025,7 @@ int sdr_stereo_pll(sdr_ctx* c, void* stream) {
 // a persistent launch the host already knows timed out (sdr_plls_report): its blocks' post stages
 // fail (the device poisons their outputs anyway, for callers that have not asked yet)
 static int check_pers_failed(const sdr_ctx* c, const char* what) {
-    if (c->pers_failed && c->post_err())
+    if (c->pers_failed && c->pers_err())
         return fail(SDR_E_HIP, "%s: the persistent PLL launch of this block timed out (outputs invalid): "
                                "sdr_ctx_reset, then a new sdr_plls_launch", what);
     return SDR_OK;
@@ -1922,6 +2033,7 @@ static int check_pers_failed(const sdr_ctx* c, const char* what) {
 
 int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
     if (!c || !lr) return fail(SDR_E_INVALID, "null argument");
+    if (const int rf_ = check_failed(c, "stereo_post")) return rf_;
     if (c->st_pll_done != c->block || c->stereo_done == c->block)
         return fail(SDR_E_INVALID, "stereo_post: run sdr_stereo_pll on a new block first");
     if (const int rf = check_pers_failed(c, "stereo_post")) return rf;
@@ -1953,7 +2065,7 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
         a.ny = in.n_audio;
         a.lr = lr;
         a.lr_stride = lr_stride;
-        a.err = c->post_err();
+        a.err = block_poison(c);
         const dim3 g(cdiv(in.n_audio, ATILE), c->nch);
         if (in.audio_decim == 5)
             hipLaunchKernelGGL(k_stereo_out<5>, g, dim3(AT), 0, s, a);
@@ -1986,11 +2098,9 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
                        c->fm_stride, c->fm_stride, c->audio_pp, c->audio_cnt, c->audio_L, in.audio_upsample,
                        in.audio_decim, in.n_audio, tile, -(HIST - 50), (void*)lr, lr_stride);
     LAUNCH_CHECK();
-    if (const uint32_t* err = c->post_err()) {
-        hipLaunchKernelGGL(k_poison_i16, dim3(cdiv(2 * in.n_audio, BLK), c->nch), dim3(BLK), 0, s, err, lr, lr_stride,
-                           2 * in.n_audio);
-        LAUNCH_CHECK();
-    }
+    hipLaunchKernelGGL(k_poison_i16, dim3(cdiv(2 * in.n_audio, BLK), c->nch), dim3(BLK), 0, s, block_poison(c), lr,
+                       lr_stride, 2 * in.n_audio);
+    LAUNCH_CHECK();
     c->stereo_done = c->block;
     return release_record(c, REL_STEREO, s);
 }
@@ -2023,6 +2133,7 @@ int rds_sq_fir(sdr_ctx* c, hipStream_t s, int x0 = 0, int xn = 0) {
 
 int sdr_rds_pre(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "rds_pre")) return rf_;
     if (c->block < 0 || c->rds_pre_done == c->block) return fail(SDR_E_INVALID, "rds_pre: no new block");
     if (c->ntaps != FRB_T) return fail(SDR_E_INVALID, "rds_pre: %d taps", c->ntaps);
     hipStream_t s = S(stream);
@@ -2065,6 +2176,7 @@ int pre_launch(sdr_ctx* c, hipStream_t s, int x0 = 0, int xn = 0) {
 
 int sdr_pre(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "pre")) return rf_;
     if (c->block < 0 || c->st_pre_done == c->block || c->rds_pre_done == c->block)
         return fail(SDR_E_INVALID, "pre: no new block");
     if (!c->rds_on) return sdr_stereo_pre(c, stream);
@@ -2078,6 +2190,7 @@ int sdr_pre(sdr_ctx* c, void* stream) {
 
 int sdr_rds_pll(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "rds_pll")) return rf_;
     if (c->rds_pre_done != c->block || c->rds_pll_done == c->block)
         return fail(SDR_E_INVALID, "rds_pll: run sdr_rds_pre on a new block first");
     PllJobs jobs{};
@@ -2090,6 +2203,7 @@ int sdr_rds_pll(sdr_ctx* c, void* stream) {
 
 int sdr_plls(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "plls")) return rf_;
     if (c->st_pre_done != c->block || c->st_pll_done == c->block || c->rds_pre_done != c->block ||
         c->rds_pll_done == c->block)
         return fail(SDR_E_INVALID, "plls: run sdr_stereo_pre and sdr_rds_pre on a new block first");
@@ -2149,7 +2263,21 @@ static int plls_prepare(sdr_ctx* c, int nblocks, hipStream_t s) {
     HIP_TRY(hipMemsetAsync(c->pers_t0, 0xFF, (size_t)nblocks * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(c->pers_t1, 0, (size_t)nblocks * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(c->pers_cyc, 0, (size_t)nblocks * 2 * sizeof(unsigned long long), s));
-    HIP_TRY(hipMemsetAsync(c->pers_words + 1, 0, sizeof(uint32_t), s));   // err of this launch
+    // err of this launch: cleared after every post stream that read the previous launch's (their
+    // queued stages would otherwise poison by a word that no longer says so, or read a clear word for a
+    // block the old launch never computed)
+    if (c->pers_nreaders > sdr_ctx::PERS_READERS) {
+        HIP_TRY(hipDeviceSynchronize());
+    } else {
+        for (int i = 0; i < c->pers_nreaders; i++) {
+            if (c->pers_readers[i] == s) continue;
+            if (!c->pers_reader_ev[i]) HIP_TRY(hipEventCreateWithFlags(&c->pers_reader_ev[i], hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(c->pers_reader_ev[i], c->pers_readers[i]));
+            HIP_TRY(hipStreamWaitEvent(s, c->pers_reader_ev[i], 0));
+        }
+    }
+    c->pers_nreaders = 0;
+    HIP_TRY(hipMemsetAsync(c->pers_words + 1, 0, sizeof(uint32_t), s));
     c->pers_prepared = nblocks;
     c->pers_prepared_launch = c->pers_launched;
     return SDR_OK;
@@ -2164,6 +2292,7 @@ int sdr_plls_prepare(sdr_ctx* c, int nblocks, void* stream) {
 
 int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_launch: bad arguments");
+    if (const int rf_ = check_failed(c, "plls_launch")) return rf_;
     if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_launch: not with SDR_FLAG_PLL_LIBM");
     hipStream_t s = S(stream);
     // the launch's waves spin until later dispatches on other streams publish each block, so the
@@ -2231,6 +2360,7 @@ int plls_signal_check(const sdr_ctx* c, long long block, const char* what) {
 
 int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int nparts, void* stream) {
     if (!c || !iq || nparts < 1) return fail(SDR_E_INVALID, "frontend_pre_parts: bad arguments");
+    if (const int rf_ = check_failed(c, "frontend_pre_parts")) return rf_;
     if (const int r = check_iq(c, iq, iq_stride)) return r;
     if (!c->rds_on || c->ntaps != FRB_T || (c->flags & SDR_FLAG_FAST_FRONTEND))
         return fail(SDR_E_INVALID, "frontend_pre_parts: needs rds_on, 101 taps and the exact front end");
@@ -2243,8 +2373,12 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
     const int p = c->parity ^ 1;
     const FrontendArgs a = frontend_args(c, iq, iq_stride, p);
     if (const int rw = release_wait(c, p, REL_MONO | REL_STEREO | REL_RDS, s)) return rw;
+    const int parity0 = c->parity;
+    const long long block0 = c->block;
     c->parity = p;                 // the block's buffers (the pre-PLL FIRs read c->parity)
     c->block++;
+    // a launch that fails part-way leaves the context on the previous block (nothing was signalled)
+    auto undo = [&](int r) { c->parity = parity0; c->block = block0; return r; };
     // part q: the FIR tiles [x0, x1) and the front-end tiles their windows need (tile j writes
     // outputs [adv j, adv j + adv), adv = 64 R - 1); after each part but the last, the count of
     // published tiles
@@ -2261,7 +2395,7 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
         if (!r && q < nparts - 1)
             r = launch_flag_store(c->pers_words + PLL_WORD_SUB,
                                   c->pers_base * PLL_SUB_SCALE + std::min((uint32_t)x1, PLL_SUB_SCALE - 1u), s);
-        if (r) return r;
+        if (r) return undo(r);
     }
     c->st_pre_done = c->rds_pre_done = c->block;
     return sdr_plls_signal(c, stream);   // the whole block: the launch's flag
@@ -2269,6 +2403,7 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
 
 int sdr_plls_signal(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "plls_signal")) return rf_;
     if (c->st_pre_done != c->block || c->rds_pre_done != c->block || c->st_pll_done == c->block ||
         c->rds_pll_done == c->block)
         return fail(SDR_E_INVALID, "plls_signal: run sdr_stereo_pre and sdr_rds_pre on a new block first");
@@ -2284,11 +2419,22 @@ int sdr_plls_signal(sdr_ctx* c, void* stream) {
 
 int sdr_plls_wait(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "plls_wait")) return rf_;
     if (c->pers_block != c->block) return fail(SDR_E_INVALID, "plls_wait: sdr_plls_signal this block first");
     // every wave has finished this block's sequence number (its slot of the done ring)
     const uint32_t seq = c->pers_block_seq;
     const uint32_t want = c->pers_waves * (seq / PLL_DONE_RING + 1u);
     if ((int32_t)(seq + 1u - c->pers_waited) > 0) c->pers_waited = seq + 1u;
+    // this stream's post stages read the launch's error word: the next prepare orders its reset after
+    // them (a post stream not in the list -- more than PERS_READERS of them -- falls back to a device
+    // synchronisation there)
+    hipStream_t ws = S(stream);
+    bool known = false;
+    for (int i = 0; i < c->pers_nreaders; i++) known |= c->pers_readers[i] == ws;
+    if (!known) {
+        if (c->pers_nreaders < sdr_ctx::PERS_READERS) c->pers_readers[c->pers_nreaders++] = ws;
+        else c->pers_nreaders = sdr_ctx::PERS_READERS + 1;   // overflow: synchronise in the prepare
+    }
     return launch_flag_wait(c->pers_words + PLL_WORDS_DONE + seq % PLL_DONE_RING, want, c->pers_words + 1, S(stream));
 }
 
@@ -2355,6 +2501,7 @@ int sdr_plls_cycles(sdr_ctx* c, double* cycles_per_step, double* clock_mhz, void
 
 int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "rds_post")) return rf_;
     if (c->rds_pll_done != c->block || c->rds_dsp_done == c->block)
         return fail(SDR_E_INVALID, "rds_post: run sdr_rds_pll on a new block first");
     if (const int rf = check_pers_failed(c, "rds_post")) return rf;
@@ -2421,7 +2568,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         f.y_stride[0] = c->clean_stride;
         f.ydup = rds_clean;
         f.ydup_stride = rds_stride;
-        f.err = c->post_err();                      // NaN rows after a persistent PLL timeout
+        f.err = block_poison(c);                    // NaN rows after a persistent PLL or release timeout
         const int r = fir_rb<1, false>(c, rfilt, c->rf_stride, in.n_rds, f, s);
         if (r) return r;
     }
@@ -2441,6 +2588,7 @@ int sdr_rds_dsp(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
 int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, size_t sym_stride, int32_t* nbits,
                  uint8_t* bits, size_t bits_stride, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
+    if (const int rf_ = check_failed(c, "rds_bits")) return rf_;
     if (c->rds_dsp_done != c->block || c->rds_bits_done == c->block)
         return fail(SDR_E_INVALID, "rds_bits: run sdr_rds_dsp on a new block first");
     if (const int rf = check_pers_failed(c, "rds_bits")) return rf;
@@ -2448,7 +2596,7 @@ int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, s
     hipLaunchKernelGGL(k_rds_bits, dim3(c->nch), dim3(64), (size_t)in.n_rds * sizeof(float),
                        S(stream), c->rds_clean,
                        c->clean_stride, in.n_rds, in.symbol_Fs, c->rds_on, c->dec, offset, nsym, symbols,
-                       sym_stride, nbits, bits, bits_stride, c->post_err(),
+                       sym_stride, nbits, bits, bits_stride, block_poison(c),
                        (reinterpret_cast<uintptr_t>(c->rds_clean) % 16 == 0 && c->clean_stride % 4 == 0) ? 1 : 0);
     LAUNCH_CHECK();
     c->rds_bits_done = c->block;
@@ -2628,6 +2776,7 @@ int sdr_differential_decode(uint8_t* out, size_t out_stride, const uint8_t* bits
 
 int sdr_push_fm_demod(sdr_ctx* c, const float* fm, size_t fm_stride, void* stream) {
     if (!c || !fm) return fail(SDR_E_INVALID, "null argument");
+    if (const int rf_ = check_failed(c, "push_fm_demod")) return rf_;
     const sdr_info& in = c->info;
     const int p = c->parity ^ 1;
     float* dst = c->fm + p * c->fm_par;

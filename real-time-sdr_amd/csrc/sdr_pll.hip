@@ -87,20 +87,11 @@ struct PllProof {
     uint32_t tie = ~0u;
     float tmax = 0.0f;
 };
-#ifndef SDR_PLL_HI_FIRST
-#define SDR_PLL_HI_FIRST 1
-#endif
-#ifndef SDR_PLL_PREWAIT
-#define SDR_PLL_PREWAIT 0
-#endif
-#ifndef SDR_PLL_LF_SCALAR
-#define SDR_PLL_LF_SCALAR 1   // the plain f32 loop filter (no inline asm): +1.2 %, profiles/r02/ab_pll_lf.txt
-#endif
-#ifndef SDR_PLL_EDHI
-#define SDR_PLL_EDHI 0
-#endif
+// (the A/B variants of this step measured and dropped -- e bracket order, bracket by fma, pre-loop
+// wait, packed loop filter, first table entries carried, one lane per chain, no trigArg table -- are
+// kept as tools/patches/pll_variants.patch)
 // |e| bound of the fast phase detector (the wrap to [-pi, pi] is the reference's below it)
-constexpr double PLL_EMAX = SDR_PLL_EDHI ? pllm::PI - 0x1p-30 - 0x1p-42 : pllm::PI - 0x1p-30;
+constexpr double PLL_EMAX = pllm::PI - 0x1p-30;
 // the largest f32 below PLL_EMAX: RN32 is monotone, so |RN32(ed)| < PLL_EMAX_F implies |ed| < PLL_EMAX_F
 constexpr float PLL_EMAX_F = __builtin_bit_cast(float, 0x40490FDAu);
 static_assert((double)PLL_EMAX_F < PLL_EMAX, "PLL_EMAX_F");
@@ -208,23 +199,11 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
     // pll.cpp:39: atan2(eQ, eI) = base + Y/X (pll_math.h phase_detect2), rounding proven below
     const double base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
     const double Y = pllm::fma_((double)eI0, r.s, (double)eQ0 * r.c);
-#if SDR_PLL_EDHI
-    // the bracket ed -/+ eps as fma(Y, rx, base -/+ eps): base -/+ eps is ready before the input,
-    // so the rounded e is one operation closer to Y (same proof: each end moves < 2^-50.5, far
-    // inside eps - |error of ed|); |ed| <= |ed + eps| + 2^-43 for the range test
-    const double ed = pllm::fma_(Y, rx, base + pllm::EPS_ABS_E2);
-    const float lo = (float)pllm::fma_(Y, rx, base - pllm::EPS_ABS_E2), hi = (float)ed;
-#else
     const double ed = pllm::fma_(Y, rx, base);
-#if SDR_PLL_HI_FIRST
-    // hi (the value used) first: the loop filter's packed product can issue while lo, the range
-    // and the split test fill its hazard wait states
+    // hi (the value used) first: the loop filter's product can issue while lo, the range and the
+    // split test fill its wait states
     const float hi = (float)(ed + pllm::EPS_ABS_E2);
     const float lo = (float)(ed - pllm::EPS_ABS_E2);
-#else
-    const float lo = (float)(ed - pllm::EPS_ABS_E2), hi = (float)(ed + pllm::EPS_ABS_E2);
-#endif
-#endif
     float e = hi;                                             // = RN32(ed) whenever lo == hi
     if (CHECKED) {
         if (!((__builtin_fabs(ed) < PLL_EMAX) && lo == hi)) {
@@ -236,23 +215,15 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
         pf.emax = fmax(pf.emax, __builtin_fabs(ed));
         pf.split = or_xor(pf.split, __builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
     }
-    // pll.cpp:41-42: integ += Ki e; phaseEst = (phaseEst + Kp e) + integ, with the two products
-    // and the two first sums as one v_pk_mul_f32 + one v_pk_add_f32 (the same f32 roundings)
-#if SDR_PLL_LF_SCALAR
-    // scalar f32: 5 VALU, and no hazard wait states after packed-f32 results
+    // pll.cpp:41-42: integ += Ki e; phaseEst = (phaseEst + Kp e) + integ, as scalar f32 (5 VALU,
+    // no hazard wait states after packed-f32 results: +1.2 % against the packed form,
+    // profiles/r02/ab_pll_lf.txt)
     {
-        float ki_e = Ki * e;
-        if (SDR_PLL_LF_SCALAR == 2) asm("" : "+v"(ki_e));      // keeps the SLP vectoriser from packing
+        const float ki_e = Ki * e;
         const float integ = r.ip.x + ki_e;
         r.ip.y = (r.ip.y + Kp * e) + integ;
         r.ip.x = integ;
     }
-#else
-    r.ip = r.ip + f32x2{Ki, Kp} * f32x2{e, e};
-    float ph = r.ip.y;                                        // in place (else a pk_add + move)
-    asm("v_add_f32 %0, %0, %1" : "+v"(ph) : "v"(r.ip.x));
-    r.ip.y = ph;
-#endif
     float t;
     if (TAB) {                                                // wt = w * trigOffset, tabulated
         t = (float)(wt + (double)r.ip.y);                     // pll.cpp:47
@@ -291,9 +262,6 @@ __device__ __forceinline__ void pll_step(PllRegs& r, float x, double rx, float K
 #define SDR_PLL_CHUNK 16
 #endif
 constexpr int PLL_CHUNK = SDR_PLL_CHUNK;
-#ifndef SDR_PLL_W01
-#define SDR_PLL_W01 0
-#endif
 #ifndef SDR_PLL_NBUF
 #define SDR_PLL_NBUF 2
 #endif
@@ -358,34 +326,15 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
     if (nmain > 0) {
 #pragma unroll
         for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
-#if SDR_PLL_PREWAIT
-        // the first buffers land before the loop (one memory latency per block). Otherwise the
-        // compiler's wait counts at the loop header merge these loads' positions with the back
-        // edge's and the steady-state loop waits for loads and stores it does not need: vmcnt(4)
-        // before every refill (the previous chunk's refill) and vmcnt(12) inside every chunk (the
-        // stores just issued), exposing a memory latency per chunk.
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt and lgkmcnt unconstrained (gfx9)
-#endif
     }
-#if SDR_PLL_W01
-    double2 w01 = TAB ? reinterpret_cast<const double2*>(wtab)[0] : double2{0.0, 0.0};
-#endif
     for (int c0 = 0; c0 < nmain; c0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; u++) {
             const int i0 = (c0 + u) * C;
             double wv[C];
             if (TAB) {
-                // the first two steps' table entries were read at the end of the previous chunk
-                // (w01), so the chunk's first steps do not wait on the LDS latency
-#if SDR_PLL_W01
-                wv[0] = w01.x; wv[1] = w01.y;
-#pragma unroll
-                for (int k = 1; k < C / 2; k++) {
-#else
 #pragma unroll
                 for (int k = 0; k < C / 2; k++) {
-#endif
                     const double2 v = reinterpret_cast<const double2*>(wtab + i0)[k];
                     wv[2 * k] = v.x; wv[2 * k + 1] = v.y;
                 }
@@ -416,9 +365,6 @@ __device__ __forceinline__ void pll_run(const PllJob& jb, int n, int ch, const d
             }
             // refill (the last refills re-read the final chunk: harmless, keeps the loop branch-free)
             load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
-#if SDR_PLL_W01
-            if (TAB) w01 = reinterpret_cast<const double2*>(wtab)[min(i0 + C, n - 2) >> 1];
-#endif
         }
     }
     {
@@ -1087,14 +1033,6 @@ __global__ __launch_bounds__(BLK) void k_nco_out(const PllJobs jobs, int n) {
 }  // namespace
 
 // compile-time A/B switches for variant builds (tools/build_variant.sh), never read at run time:
-// SDR_PLL_NOSPLIT=1 one lane per channel even where the producer wrote -x (the lane pairs off),
-// SDR_PLL_NOTAB=1 per-lane trigArg offsets (the LDS table off)
-#ifndef SDR_PLL_NOSPLIT
-#define SDR_PLL_NOSPLIT 0
-#endif
-#ifndef SDR_PLL_NOTAB
-#define SDR_PLL_NOTAB 0
-#endif
 
 int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
     if (n > 0) {
@@ -1105,7 +1043,7 @@ int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s) {
 }
 
 int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s, bool with_nco) {
-    bool vec = true, split = !SDR_PLL_NOSPLIT;
+    bool vec = true, split = true;
     for (int k = 0; k < njobs; k++) {
         const PllJob& j = jobs.j[k];
         vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
@@ -1117,7 +1055,7 @@ int launch_plls(bool libm, const PllJobs& jobs, int njobs, int n, int nch, hipSt
     const dim3 g(cdiv(split ? 2 * nch : nch, 64), njobs), b(64);
     // LDS table of w * trigOffset (k_pll): n doubles, 16-byte rows
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
-    const int tab_ok = (tab_bytes <= 64 * 1024 && !SDR_PLL_NOTAB) ? 1 : 0;
+    const int tab_ok = tab_bytes <= 64 * 1024 ? 1 : 0;
     const size_t lds = tab_ok ? tab_bytes : 0;
     if (libm) {
         hipLaunchKernelGGL(k_pll_libm, g, b, 0, s, jobs, n, nch);
@@ -1149,7 +1087,7 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
                      hipStream_t s, int max_cus, int sub_tile) {
-    bool vec = true, split = !SDR_PLL_NOSPLIT;
+    bool vec = true, split = true;
     for (int k = 0; k < 2; k++)
         for (int q = 0; q < 2; q++) {
             const PllJob& j = jobs.p[k].j[q];
@@ -1160,7 +1098,7 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
             split = split && j.in_neg;
         }
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
-    const int tab_ok = (tab_bytes <= 64 * 1024 && !SDR_PLL_NOTAB) ? 1 : 0;
+    const int tab_ok = tab_bytes <= 64 * 1024 ? 1 : 0;
     const size_t lds = tab_ok ? tab_bytes : 0;
     const int wave_cnt = cdiv(split ? 2 * nch : nch, 64) * 2;
     // one wave per workgroup (its own CU time slice and table) while two tables per CU fit the

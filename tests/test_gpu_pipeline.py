@@ -463,6 +463,18 @@ def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda, own_qu
         assert (pipe.nbits.cpu().numpy() == pkg.SDR_NBITS_POISONED).all(), "late block: nbits not poisoned"
         with pytest.raises(pkg.SdrError, match="timed out"):
             pipe.plls_report(stream=s_pll)
+        # a reset context run with per-block PLL dispatches: the block whose index the timed-out
+        # launch last signalled (2) reads no stale error word (pers_block kept by reset)
+        pipe.reset()
+        for b in range(nb):
+            pipe.frontend(d[b])
+            pipe.pre()
+            pipe.plls()
+            pipe.stereo_post(lr)
+            pipe.rds_post(clean, bits=True)
+            assert np.array_equal(lr.cpu().numpy(), ref["stereo"][b]), f"dispatch after reset: stereo block {b}"
+            assert np.array_equal(clean.cpu().numpy().view(np.uint32), ref["clean"][b].view(np.uint32))
+            assert np.array_equal(pipe.nbits.cpu().numpy(), ref["nbits"][b])
         # recovery: reset the state the poisoned launch left, a new launch, block 0 again
         pipe.reset()
         pipe.plls_launch(1, stream=s_pll)
@@ -470,6 +482,74 @@ def test_persistent_plls_missing_signal_times_out(pkg, synth, torch_cuda, own_qu
         assert np.array_equal(lr.cpu().numpy(), ref["stereo"][0]), "stereo after recovery"
         assert np.array_equal(clean.cpu().numpy().view(np.uint32), ref["clean"][0].view(np.uint32))
         assert len(pipe.plls_report(stream=s_pll)) == 1
+    pipe.close()
+
+
+def test_release_timeout_poisons_and_fails(pkg, synth, torch_cuda):
+    """A reader that never releases its block (the parity-release wait, include/sdr_amd.h): block 0's
+    mono, stereo post and RDS post are queued on a stream held by a one-wave kernel for 6.5 s, so
+    block 2's front end -- the same buffer parity -- waits the bounded 5 s for them and then goes on.
+    That is an error, never wrong output (the reference's producer never overwrites a slot its
+    consumers hold, /root/reference/include/threadsafequeue.h:24-44): the late readers, which would
+    read block 2's fm_demod, and every output stage after the timeout write SDR_PCM_POISON audio, NaN
+    rds_clean and nbits = SDR_NBITS_POISONED; every later call returns SDR_E_TIMEOUT; sdr_ctx_reset
+    recovers (block 0 again, bit-exact)."""
+    import ctypes as C
+    torch = torch_cuda
+    nch, nb = 8, 3
+    iqs = [channel_input(synth, 600 + c, nb) for c in range(nch)]
+    d = torch.from_numpy(np.stack(iqs, axis=1)).cuda()
+    ref = _run_pipeline(pkg, torch, iqs, 1)
+    pipe = pkg.Pipeline(nch)
+    L = pkg.lib()
+    L.sdr_diag_hold.argtypes = [C.c_void_p, C.c_int]
+    L.sdr_diag_hold.restype = C.c_int
+    info = pipe.info
+    s_fe, s_rd = torch.cuda.Stream(), torch.cuda.Stream()
+    mono = [torch.zeros(nch, info.n_audio, dtype=torch.int16, device="cuda") for _ in range(nb)]
+    lr = [torch.zeros(nch, 2 * info.n_audio, dtype=torch.int16, device="cuda") for _ in range(nb)]
+    clean = [torch.zeros(nch, info.n_rds, dtype=torch.float32, device="cuda") for _ in range(nb)]
+    bits = [torch.zeros(nch, pkg.SDR_MAX_BITS, dtype=torch.uint8, device="cuda") for _ in range(nb)]
+    torch.cuda.synchronize()
+    # block 0 on s_fe; its three readers on s_rd, behind the hold
+    pipe.frontend(d[0], stream=s_fe)
+    pipe.pre(stream=s_fe)
+    pipe.plls(stream=s_fe)
+    ev = torch.cuda.Event()
+    ev.record(s_fe)
+    s_rd.wait_event(ev)
+    pkg.check(L.sdr_diag_hold(C.c_void_p(s_rd.cuda_stream), 6500), "sdr_diag_hold")
+    pipe.mono(mono[0], stream=s_rd)
+    pipe.stereo_post(lr[0], stream=s_rd)
+    pipe.rds_post(clean[0], bits=True, stream=s_rd, bits_out=bits[0])
+    # block 1: produced, not read; block 2 reuses block 0's parity and waits for its readers
+    pipe.frontend(d[1], stream=s_fe)
+    pipe.pre(stream=s_fe)
+    pipe.plls(stream=s_fe)
+    pipe.frontend(d[2], stream=s_fe)
+    pipe.mono(mono[2], stream=s_fe)
+    pipe.pre(stream=s_fe)
+    pipe.plls(stream=s_fe)
+    pipe.stereo_post(lr[2], stream=s_fe)
+    pipe.rds_post(clean[2], bits=True, stream=s_fe, bits_out=bits[2])
+    torch.cuda.synchronize()    # ~6.5 s: the wait gave up at 5 s, the held readers ran after it
+    for b in (0, 2):
+        assert (mono[b].cpu().numpy() == pkg.SDR_PCM_POISON).all(), f"block {b}: mono not poisoned"
+        assert (lr[b].cpu().numpy() == pkg.SDR_PCM_POISON).all(), f"block {b}: stereo not poisoned"
+        assert np.isnan(clean[b].cpu().numpy()).all(), f"block {b}: rds_clean not poisoned"
+    assert (pipe.nbits.cpu().numpy() == pkg.SDR_NBITS_POISONED).all(), "nbits not poisoned"
+    with pytest.raises(pkg.SdrError, match="release wait timed out") as ei:
+        pipe.frontend(d[0], stream=s_fe)
+    assert ei.value.code == pkg.SDR_E_TIMEOUT
+    with pytest.raises(pkg.SdrError) as ei:
+        pipe.mono(mono[1], stream=s_fe)
+    assert ei.value.code == pkg.SDR_E_TIMEOUT
+    # recovery
+    pipe.reset()
+    pipe.frontend(d[0])
+    assert np.array_equal(pipe.mono().cpu().numpy(), ref["mono"][0]), "mono after reset"
+    assert np.array_equal(pipe.stereo().cpu().numpy(), ref["stereo"][0]), "stereo after reset"
+    assert np.array_equal(pipe.rds().cpu().numpy().view(np.uint32), ref["clean"][0].view(np.uint32))
     pipe.close()
 
 

@@ -21,6 +21,8 @@ def main() -> None:
     ap.add_argument("--channels", type=int, default=2048)
     ap.add_argument("--n", type=int, default=7350)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--cus", type=int, default=0,
+                    help="run on a stream CU-masked to CUs [0, cus) (waves per CU = waves / cus)")
     args = ap.parse_args()
     import torch
     pkg = bench._load_pkg()
@@ -32,7 +34,11 @@ def main() -> None:
     x = x + 0.01 * torch.randn(nch, n, device=dev)
     out = torch.empty(nch, n + 1, dtype=torch.float32, device=dev)
     st = pkg.pll_state_tensor(nch, device=dev)
-    s = torch.cuda.Stream(dev)
+    created = []
+    if args.cus > 0:
+        s = bench.cu_masked_streams(torch, pkg, dev, str(args.cus), created, all_cus=False)[1]
+    else:
+        s = torch.cuda.Stream(dev)
     for _ in range(2):
         pkg.fmpll(out, x, 19e3, 240e3, st, 2.0, 0.0, 0.01, stream=s)
     torch.cuda.synchronize()
@@ -43,8 +49,9 @@ def main() -> None:
     e1.record(s)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters
-    print(json.dumps({"channels": nch, "steps": n, "ms_per_call": round(ms, 4),
+    print(json.dumps({"channels": nch, "steps": n, "cus": args.cus or None, "ms_per_call": round(ms, 4),
                       "ns_per_step": round(ms * 1e6 / n, 2)}))
+    bench.destroy_masked_streams(torch, pkg, dev, created)
 
 
 if __name__ == "__main__":
