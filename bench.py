@@ -245,6 +245,9 @@ class GpuStepper:
     def prepare_phase(self, nblocks: int) -> None:
         """Before the timer: the persistent launch's bookkeeping (stamp arrays reset), so the timed
         region starts with the launch and the first front end instead of four memsets."""
+        # the front-end kernels of the timed blocks record their own dispatch stamps (the roofline's
+        # average launch time: the kernel alone, as a rocprofv3 kernel trace times it)
+        self.pipe.frontend_timing(nblocks)
         if self.persist:
             self.pipe.plls_prepare(nblocks, stream=self.s_pll)
             self.torch.cuda.synchronize(self.dev)
@@ -397,9 +400,15 @@ class GpuStepper:
         """Kernel-level timings of the timed blocks (HIP events on the launching streams)."""
         info, nch = self.info, self.nch
         rng = range(warmup, self.nblocks)
-        # the front end's own launch time; a block whose front end ran in parts (the fill) has none
-        fe_avg_s = float(np.mean([self.fe_start[b].elapsed_time(self.fe_end[b]) for b in rng
-                                  if b != self.parts_block])) / 1e3
+        # the front-end kernel's own time per launch: earliest workgroup start to latest workgroup end
+        # (sdr_frontend_timing, armed in prepare_phase); a block whose front end ran in parts (the
+        # fill) has none. Without them, the HIP events around each launch on its stream.
+        fe_ms = self.pipe.frontend_times()
+        fe_src = "the kernel's own workgroup start/end stamps (sdr_frontend_timing)"
+        if not fe_ms:
+            fe_ms = [self.fe_start[b].elapsed_time(self.fe_end[b]) for b in rng if b != self.parts_block]
+            fe_src = "HIP events around each launch"
+        fe_avg_s = float(np.mean(fe_ms)) / 1e3
         fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)     # u8 I/Q in + f32 fm_demod out
         cyc = None
         timeline = None
@@ -435,7 +444,8 @@ class GpuStepper:
             "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": _pmc_traffic(nch, self.args.numerics),
-                         "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4)},
+                         "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg_s * 1e3, 4),
+                         "launches_timed": len(fe_ms), "timed_by": fe_src},
             "pll": {"kernel": ("k_pll_multi: persistent, all blocks of the phase in one dispatch" if self.persist
                                else "k_pll: one dispatch per block") +
                               ", stereo 19 kHz + RDS 114 kHz PLLs (pll.cpp:4-61), 2 x channels serial chains",
@@ -878,8 +888,9 @@ def _blob(channel: int, nblocks: int) -> bytes:
     return b"".join(src.next_block().tobytes() for _ in range(nblocks))
 
 
-def _run_reference(exe, blob: bytes, reps: int) -> float:
-    """Pipe `reps` copies of blob through `project 0 r`; returns the wall seconds."""
+def _run_reference(exe, blob: bytes, reps: int, keep: bool = False):
+    """Pipe `reps` copies of blob through `<exe> 0 r`; returns the wall seconds (and, with keep, the
+    program's stdout: its PCM)."""
     with tempfile.TemporaryFile() as out:
         t0 = time.perf_counter()
         p = subprocess.Popen([str(exe), "0", "r"], stdin=subprocess.PIPE, stdout=out, stderr=subprocess.DEVNULL)
@@ -890,7 +901,34 @@ def _run_reference(exe, blob: bytes, reps: int) -> float:
         except BrokenPipeError:
             pass
         p.wait()
-        return time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        if not keep:
+            return dt
+        out.seek(0)
+        return dt, out.read()
+
+
+def _dropin_leg(gpu_exe, blob: bytes, reps: int, nblk: int, dt_ref: float, pcm_ref: bytes) -> dict:
+    """The unchanged program on the GPU: the reference's own src/project.cpp linked against
+    libsdr_host.so (oracle/_ref/project_gpu: its three stage threads over the C ABI, one channel),
+    `project_gpu 0 r` on the same stdin as the reference's `project 0 r`, timed beside it; its PCM is
+    compared with the reference program's over their common length (both end by exit(1) on EOF,
+    rffrontend.cpp:50-52, which can cut the last blocks of either)."""
+    synth = _synth_module()
+    dt, pcm = _run_reference(gpu_exe, blob, reps, keep=True)
+    n = min(len(pcm), len(pcm_ref))
+    per_block = 2 * 2 * synth.BLOCK_IQ // 50          # stereo int16 frames of one block (2940 x 2 B)
+    samples = reps * nblk * synth.BLOCK_IQ
+    rt = samples / 2.4e6                               # the input's duration at 2.4 MS/s
+    return {"value": round(samples / dt / 1e6, 3), "unit": "MS/s", "kind": "dropin",
+            "real_time_factor": round(rt / dt, 1), "wall_s": round(dt, 3),
+            "reference_value": round(samples / dt_ref / 1e6, 3), "reference_wall_s": round(dt_ref, 3),
+            "speedup_vs_reference": round(dt_ref / dt, 3),
+            "pcm_equal_blocks": n // per_block if pcm[:n] == pcm_ref[:n] else -1,
+            "blocks": reps * nblk,
+            "sample": f"the reference's unmodified src/project.cpp linked against libsdr_host.so "
+                      f"(oracle/_ref/project_gpu 0 r: 3 stage threads, 1 channel on the GPU) on the same "
+                      f"{reps * nblk} blocks via stdin as the reference `project 0 r` run beside it"}
 
 
 def _check_channel(job):
@@ -984,12 +1022,18 @@ def cpu_baseline_leg(args, cap: dict | None, timing: bool = True) -> dict:
         nblk = 32
         blob = _blob(0, nblk)
         reps = 150  # 4800 blocks = 353 M I/Q samples (~10 s at the reference's ~37 MS/s)
-        dt = _run_reference(exe, blob, reps)
+        dt, pcm_ref = _run_reference(exe, blob, reps, keep=True)
         res.update({"value": round(reps * nblk * synth.BLOCK_IQ / dt / 1e6, 3), "unit": "MS/s", "cores": 3,
                     "kind": "reference",
                     "sample": f"reference `project 0 r` (src/*.cpp, g++ -O3, 3 threads RF/audio/RDS) on "
                               f"{reps * nblk} blocks = {reps * nblk * synth.BLOCK_IQ / 1e6:.1f} M I/Q samples of "
                               f"1 channel via stdin, {dt:.2f} s wall"})
+        gpu_exe = ROOT / "oracle" / "_ref" / "project_gpu"
+        if gpu_exe.exists() and os.environ.get("SDR_BENCH_DROPIN", "1") != "0":
+            try:
+                res["dropin_1ch"] = _dropin_leg(gpu_exe, blob, reps, nblk, dt, pcm_ref)
+            except (OSError, subprocess.SubprocessError) as exc:
+                res["dropin_1ch"] = {"error": str(exc)}
         nproc = max(1, cores // 3)
         v, dt2 = _reference_concurrent(exe, nproc, 8, 400)     # per process: 3200 blocks of its own channel
         res["all_cores"] = {"value": round(v, 3), "unit": "MS/s", "cores": 3 * nproc, "kind": "reference",

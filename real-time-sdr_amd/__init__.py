@@ -82,6 +82,8 @@ def lib() -> C.CDLL:
         "sdr_ctx_info": ([vp, C.POINTER(Info)], i32),
         "sdr_frontend": ([vp, vp, sz, vp], i32),
         "sdr_frontend_release_wait": ([vp, vp], i32),
+        "sdr_frontend_timing": ([vp, i32], i32),
+        "sdr_frontend_times": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32)], i32),
         "sdr_mono": ([vp, vp, sz, vp], i32),
         "sdr_stereo": ([vp, vp, sz, vp], i32),
         "sdr_rds_dsp": ([vp, vp, sz, vp], i32),
@@ -289,6 +291,17 @@ class Pipeline:
         """The parity-release wait of the next frontend(), enqueued now on `stream` (that call then
         enqueues none there): the front-end kernel can be timed alone."""
         check(lib().sdr_frontend_release_wait(self._h, _stream(stream)), "sdr_frontend_release_wait")
+
+    def frontend_timing(self, max_launches: int):
+        """Record the dispatch start / end of the next max_launches frontend() kernels."""
+        check(lib().sdr_frontend_timing(self._h, max_launches), "sdr_frontend_timing")
+
+    def frontend_times(self, max_launches: int = 4096) -> list:
+        """ms per timed frontend() kernel, in call order (synchronises with the last)."""
+        arr = (C.c_double * max_launches)()
+        n = C.c_int(0)
+        check(lib().sdr_frontend_times(self._h, arr, max_launches, C.byref(n)), "sdr_frontend_times")
+        return list(arr[:n.value])
 
     def fm_demod(self, out=None, stream=None):
         import torch

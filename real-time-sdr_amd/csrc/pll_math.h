@@ -364,6 +364,23 @@ PLLM_HD SinCosRN sincos_rn(float t) {
     return o;
 }
 
+// RN_f32(cos a) of an f32 argument (the NCO output, pll.cpp:52) from the sincos_rn reduction and
+// kernels: cos(q pi/2 + r) = cos r, -sin r, -cos r, sin r for q = 0, 1, 2, 3 (mod 4), so only the
+// selected kernel's f32 rounding needs its tie proof (one key instead of two; sincos_f32 also
+// reduced in three fmas and evaluated fdlibm's longer sin). ok: the result is RN_f32(cos a), i.e.
+// |a| < T_MAX and the selected value is more than 128 f64 ulps from an f32 tie (the sin kernel's
+// error is <= 46 ulps, the cos kernel's far less; tools/pllmath/validate_nco.cpp checks it against
+// glibc). Otherwise the caller recomputes (double-double, pll_math.h dd_sincos_f32).
+PLLM_HD float cos_rn_f32(float a, bool& ok) {
+    const SinCosRN sc = sincos_rn(a);
+    const uint32_t q = 1u - sc.nq1;
+    double v = (q & 1u) ? sc.sr : sc.cr;
+    const uint32_t key = tie_key64(v);
+    if (((q + 1u) >> 1) & 1u) v = -v;                     // RN_f32 is odd: the sign after the test
+    ok = (__builtin_fabs((double)a) < T_MAX) && key > TIE_MIN;
+    return (float)v;
+}
+
 PLLM_HD double base_angle_n(uint32_t nlo, uint32_t nq1, uint32_t b, double mr) {
     const int m = (int)((nlo + nq1 + b) & 3u) - (int)(b + 1u);
     return fma_((double)m, PIO2, mr);

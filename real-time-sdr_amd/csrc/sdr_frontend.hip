@@ -5,6 +5,8 @@
 // division. Fast mode (k_frontend_mfma): the FIR as an int8 Toeplitz GEMM on the matrix cores.
 #include "sdr_internal.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -337,8 +339,11 @@ __global__ __launch_bounds__(64) void k_frontend2(
     uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
     const float* __restrict__ hs, int block_iq, int block_if,
     float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int j0, int jn,
-    const uint32_t* __restrict__ pad) {
+    const uint32_t* __restrict__ pad, unsigned long long* __restrict__ stamps) {
     constexpr int NT = 101, HP = NT - 1, NTH = 64;
+    // sdr_frontend_timing: this workgroup's start and end on the 100 MHz clock (the launch's span is
+    // the earliest start to the latest end, computed on the host)
+    if (stamps && threadIdx.x == 0) stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     constexpr int TILE = NTH * R;
     constexpr int ADV = TILE - 1;
     constexpr int WIN = (TILE - 1) * D + NT;          // staged samples (u8 I/Q pairs)
@@ -491,6 +496,10 @@ __global__ __launch_bounds__(64) void k_frontend2(
         const float* o = fm_other + (size_t)ch * fm_stride;
         for (int i = t; i < HIST; i += NTH) out[i - HIST] = o[block_if - HIST + i];
     }
+    if (stamps) {   // the end: after this wave's stores have completed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 size_t frontend_lds_bytes(int ntaps, int tile, int D) {
@@ -520,9 +529,13 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0, int jn) {
     if (jn <= 0) { j0 = 0; jn = tiles_ch; }
     if (j0 < 0 || j0 + jn > tiles_ch) return fail(SDR_E_INVALID, "frontend: tiles [%d, %d) of %d", j0, j0 + jn, tiles_ch);
     const dim3 g2(jn * a.nch);
-#define FE2(DD)                                                                                            \
-    hipLaunchKernelGGL((k_frontend2<FE_R, DD>), g2, dim3(64), 0, s, iq, iq_stride, tail_in, tail_out, prev_in, \
-                       prev_out, a.hs, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride, j0, jn, a.pad80)
+    // sdr_frontend_timing: k_frontend2 stamps each workgroup's start and end (a.stamps); the other
+    // front ends record HIP events with the launch (hipExtLaunchKernelGGL: the start event is a marker
+    // ahead of the dispatch, so its span exceeds the kernel's by the marker's latency, ~9 us)
+#define FE2(DD)                                                                                               \
+    hipExtLaunchKernelGGL((k_frontend2<FE_R, DD>), g2, dim3(64), 0, s, a.ev0, a.ev1, 0, iq, iq_stride, tail_in, \
+                          tail_out, prev_in, prev_out, a.hs, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride, j0, jn, \
+                          a.pad80, a.stamps)
     if (a.fast) {
         if (j0 != 0 || jn != tiles_ch) return fail(SDR_E_INVALID, "frontend: parts need the exact front end");
         const v4i* af = static_cast<const v4i*>(a.afrag);
@@ -530,9 +543,10 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0, int jn) {
         const bool x4 = (iq_stride % 16 == 0) && (reinterpret_cast<uintptr_t>(iq) % 16 == 0);
         constexpr int NB = FT_NB;
 #define FEM(DD, XX)                                                                                          \
-        hipLaunchKernelGGL((k_frontend_mfma<DD, XX, NB>), dim3(cdiv(a.block_if, ft_adv(DD, NB)) * a.nch), dim3(64), \
-                           0, s, iq, iq_stride, tail_in, tail_out, prev_in, prev_out, af, a.yscale, a.block_iq,    \
-                           a.block_if, fm_p, fm_o, a.fm_stride, cdiv(a.block_if, ft_adv(DD, NB)), a.pad80)
+        hipExtLaunchKernelGGL((k_frontend_mfma<DD, XX, NB>), dim3(cdiv(a.block_if, ft_adv(DD, NB)) * a.nch),   \
+                              dim3(64), 0, s, a.ev0, a.ev1, 0, iq, iq_stride, tail_in, tail_out, prev_in, prev_out, af, \
+                              a.yscale, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride,                            \
+                              cdiv(a.block_if, ft_adv(DD, NB)), a.pad80)
         if (a.D == 10) { if (x4) FEM(10, true); else FEM(10, false); }
         else if (a.D == 4) { if (x4) FEM(4, true); else FEM(4, false); }
         else { if (x4) FEM(3, true); else FEM(3, false); }
@@ -548,8 +562,9 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0, int jn) {
         const int tile = FIR_TILE;
         dim3 grid(cdiv(a.block_if, tile), a.nch);
         const size_t lds = frontend_lds_bytes(a.ntaps, tile, a.D);
-        hipLaunchKernelGGL(k_frontend, grid, dim3(BLK), lds, s, iq, iq_stride, tail_in, tail_out, prev_in,
-                           prev_out, a.h, a.ntaps, a.D, a.block_iq, a.block_if, tile, fm_p, fm_o, a.fm_stride);
+        hipExtLaunchKernelGGL(k_frontend, grid, dim3(BLK), (uint32_t)lds, s, a.ev0, a.ev1, 0, iq, iq_stride, tail_in,
+                              tail_out, prev_in, prev_out, a.h, a.ntaps, a.D, a.block_iq, a.block_if, tile, fm_p, fm_o,
+                              a.fm_stride);
     }
 #undef FE2
     LAUNCH_CHECK();

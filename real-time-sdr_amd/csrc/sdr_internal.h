@@ -103,6 +103,8 @@ struct FrontendArgs {
     double yscale;             // MFMA fixed-point scale
     const uint32_t* pad80;     // 64 words of u8 128
     bool fast;
+    hipEvent_t ev0, ev1;       // non-null: HIP events recorded with the launch (sdr_frontend_timing)
+    unsigned long long* stamps;   // non-null (k_frontend2): [workgroup][start, end] on the 100 MHz clock
 };
 // the whole block (jn <= 0) or tiles [j0, j0 + jn) of every channel (exact front end only)
 int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0 = 0, int jn = 0);
@@ -227,6 +229,12 @@ struct sdr_ctx {
     uint32_t* fail_words = nullptr;
     uint32_t* fail_host = nullptr;                      // hipHostMalloc'd (coherent), host view
     uint32_t* fail_host_dev = nullptr;                  // its device address
+    // sdr_frontend_timing: the dispatch stamps of the next fe_time_cap whole-block front-end launches
+    std::vector<hipEvent_t> fe_ev;                      // [2 * cap]: start, end per launch (HIP events)
+    unsigned long long* fe_stamps = nullptr;            // [cap][fe_stamp_wgs][2] (k_frontend2's own stamps)
+    int fe_stamp_wgs = 0, fe_stamp_cap = 0;
+    bool fe_use_stamps = false;                         // the exact front end (k_frontend2): stamps
+    int fe_time_cap = 0, fe_time_n = 0;
     std::vector<void*> allocs;
 
     float* fm_cur() const { return fm + parity * fm_par; }

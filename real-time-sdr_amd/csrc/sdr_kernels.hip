@@ -510,6 +510,62 @@ __device__ __forceinline__ void lc_group(const float* __restrict__ xr, const flo
     }
 }
 
+// The same four outputs with the tap rows read by hand-issued scalar loads from the polyphase table
+// (hr[k]: row of output k, wave-uniform) instead of LDS broadcasts: the rows are wave-uniform
+// operands, so they need no LDS (the tile's x window alone fits three workgroups per CU instead of
+// two) and no LDS bandwidth (the 16-byte broadcasts were most of the kernel's LDS traffic). Chunks
+// of 4 taps of the 4 rows, one chunk ahead (scalar loads return out of order: every wait is
+// lgkmcnt(0), as in k_fir_rb).
+template <int D1, int D2, int D3>
+__device__ __forceinline__ void lc_group_s(const float* __restrict__ xr, const float* h0, const float* h1,
+                                           const float* h2, const float* h3, float (&acc)[4]) {
+    constexpr int NW = D3 + 101;
+    constexpr int DK[4] = {0, D1, D2, D3};
+    constexpr int TC = 4, NC = 104 / TC;                   // rows padded past 101 (the table has slack)
+    typedef float f4v __attribute__((ext_vector_type(TC)));
+    float w[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) w[i] = xr[i];
+#pragma unroll
+    for (int k = 0; k < 4; k++) acc[k] = 0.0f;
+    const float* hr[4] = {h0, h1, h2, h3};
+    f4v buf[2][4];
+    auto load = [&](f4v& d, const float* hp, int c) {
+        asm volatile("s_load_dwordx4 %0, %1, %2" : "=s"(d) : "s"(hp), "s"(c * TC * 4) : "memory");
+    };
+#pragma unroll
+    for (int k = 0; k < 4; k++) load(buf[0][k], hr[k], 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 4; k++) asm volatile("" : "+s"(buf[0][k]));   // no tap use above the wait
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+#pragma unroll
+        for (int kk = 0; kk < TC; kk++) {
+            const int j = c * TC + kk;
+            if (j < 101) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) acc[k] = acc[k] + buf[c & 1][k][kk] * w[DK[k] + 100 - j];   // filter.cpp:139-141
+            }
+            if (kk == 0 && c + 1 < NC) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < 4; k++) load(buf[(c + 1) & 1][k], hr[k], c + 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (c + 1 < NC) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // chunk c + 1 landed
+#pragma unroll
+            for (int k = 0; k < 4; k++) asm volatile("" : "+s"(buf[(c + 1) & 1][k]));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) asm volatile("" : "+v"(acc[k]));
+}
+
 template <int NTAP>   // > 0: every polyphase row has exactly NTAP taps (fully unrolled sums)
 __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x, size_t x_stride, int hist_lo,
                                                      const float* __restrict__ hp, const int* __restrict__ cnt,
@@ -527,8 +583,10 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
     const int W = (ptq[n0 + nn - 1] >> 8) - qlo + 1;
     const int SW = W | 1;
     const int L4 = (L + 3) & ~3;
+    // NTAP == 101: the tap rows come from the table by scalar loads (lc_group_s), not from LDS
+    constexpr bool STAGE_TAPS = NTAP != 101;
     float* sx = smem;                                        // [64][SW]
-    float* sh = smem + ((64 * SW + 3) & ~3);                 // [RLC_TN][L4]
+    float* sh = smem + ((64 * SW + 3) & ~3);                 // [RLC_TN][L4] (STAGE_TAPS)
     // staging with every load of a wave in flight before its LDS writes: rows c = wave + 4u of the
     // x tile (lanes along the row, RLC_XL loads per row), then the polyphase rows of the outputs
     {
@@ -547,15 +605,17 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
         // the polyphase rows' loads go out with the x tile's, before any LDS write waits for them
         // (one round of global-memory latency per workgroup instead of two)
         float hv[PW][RLC_HL];
+        if (STAGE_TAPS) {
 #pragma unroll
-        for (int o8 = 0; o8 < PW; o8++) {
-            const int o = min(wave * PW + o8, nn - 1);
-            const int ph = ptq[n0 + o] & 255;
-            const int cn = cnt[ph];
+            for (int o8 = 0; o8 < PW; o8++) {
+                const int o = min(wave * PW + o8, nn - 1);
+                const int ph = ptq[n0 + o] & 255;
+                const int cn = cnt[ph];
 #pragma unroll
-            for (int k = 0; k < RLC_HL; k++) {
-                const int j = lane + 64 * k;
-                hv[o8][k] = (j < cn) ? hp[(size_t)ph * L + j] : 0.0f;
+                for (int k = 0; k < RLC_HL; k++) {
+                    const int j = lane + 64 * k;
+                    hv[o8][k] = (j < cn) ? hp[(size_t)ph * L + j] : 0.0f;
+                }
             }
         }
 #pragma unroll
@@ -567,13 +627,15 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
                 if (i < W) sx[c * SW + i] = v[u][k];
             }
         }
+        if (STAGE_TAPS) {
 #pragma unroll
-        for (int o8 = 0; o8 < PW; o8++) {
-            const int o = wave * PW + o8;
+            for (int o8 = 0; o8 < PW; o8++) {
+                const int o = wave * PW + o8;
 #pragma unroll
-            for (int k = 0; k < RLC_HL; k++) {
-                const int j = lane + 64 * k;
-                if (o < nn && j < L4) sh[o * L4 + j] = hv[o8][k];
+                for (int k = 0; k < RLC_HL; k++) {
+                    const int j = lane + 64 * k;
+                    if (o < nn && j < L4) sh[o * L4 + j] = hv[o8][k];
+                }
             }
         }
     }
@@ -595,13 +657,17 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
                 const int d1 = (ptq[n0 + o + 1] >> 8) - q0, d2 = (ptq[n0 + o + 2] >> 8) - q0,
                           d3 = (ptq[n0 + o + 3] >> 8) - q0;
                 const float* xr = sx + lane * SW + (q0 - qlo) - 100;   // xr[i] = x[q0 - 100 + i]
-                const float* hr = sh + o * L4;
+                // the 4 outputs' polyphase rows in the table (wave-uniform addresses)
+                const float* h0 = hp + (size_t)__builtin_amdgcn_readfirstlane((ptq[n0 + o] & 255) * L);
+                const float* h1 = hp + (size_t)__builtin_amdgcn_readfirstlane((ptq[n0 + o + 1] & 255) * L);
+                const float* h2 = hp + (size_t)__builtin_amdgcn_readfirstlane((ptq[n0 + o + 2] & 255) * L);
+                const float* h3 = hp + (size_t)__builtin_amdgcn_readfirstlane((ptq[n0 + o + 3] & 255) * L);
                 float acc4[4];
                 done = true;
-                if (d1 == 3 && d2 == 5 && d3 == 8) lc_group<3, 5, 8>(xr, hr, L4, acc4);
-                else if (d1 == 2 && d2 == 5 && d3 == 7) lc_group<2, 5, 7>(xr, hr, L4, acc4);
-                else if (d1 == 2 && d2 == 5 && d3 == 8) lc_group<2, 5, 8>(xr, hr, L4, acc4);
-                else if (d1 == 3 && d2 == 6 && d3 == 8) lc_group<3, 6, 8>(xr, hr, L4, acc4);
+                if (d1 == 3 && d2 == 5 && d3 == 8) lc_group_s<3, 5, 8>(xr, h0, h1, h2, h3, acc4);
+                else if (d1 == 2 && d2 == 5 && d3 == 7) lc_group_s<2, 5, 7>(xr, h0, h1, h2, h3, acc4);
+                else if (d1 == 2 && d2 == 5 && d3 == 8) lc_group_s<2, 5, 8>(xr, h0, h1, h2, h3, acc4);
+                else if (d1 == 3 && d2 == 6 && d3 == 8) lc_group_s<3, 6, 8>(xr, h0, h1, h2, h3, acc4);
                 else done = false;
                 if (done) {
 #pragma unroll
@@ -615,7 +681,7 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
                     if (o + k < nn) {
                         const int e = ptq[n0 + o + k];
                         const float* xr = sx + lane * SW + ((e >> 8) - qlo);
-                        const float* hr = sh + (o + k) * L4;
+                        const float* hr = hp + (size_t)(e & 255) * L;   // (the table: taps are not staged)
                         for (int j = 0; j < 101; j++) acc = acc + hr[j] * xr[-j];
                     }
                     out[4 * g + k] = acc;
@@ -662,9 +728,9 @@ int resample_lc_span(int L, int U, int D) {   // samples a tile reads: q span + 
     return (int)(((long long)(RLC_TN - 1) * D + U - 1) / U) + 1 + L;
 }
 
-size_t resample_lc_lds_bytes(int L, int U, int D) {
+size_t resample_lc_lds_bytes(int L, int U, int D, bool stage_taps) {
     const int W = resample_lc_span(L, U, D);
-    return (size_t)((((64 * (W | 1)) + 3) & ~3) + RLC_TN * ((L + 3) & ~3)) * sizeof(float);
+    return (size_t)((((64 * (W | 1)) + 3) & ~3) + (stage_taps ? RLC_TN * ((L + 3) & ~3) : 0)) * sizeof(float);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1771,6 +1837,8 @@ int sdr_ctx_destroy(sdr_ctx* c) {
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->fail_host) (void)hipHostFree(c->fail_host);
     if (c->pers_ev) (void)hipEventDestroy(c->pers_ev);
+    for (hipEvent_t e : c->fe_ev) (void)hipEventDestroy(e);
+    if (c->fe_stamps) (void)hipFree(c->fe_stamps);
     for (hipEvent_t e : c->pers_reader_ev)
         if (e) (void)hipEventDestroy(e);
     delete c;
@@ -1894,10 +1962,82 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
     // has nothing left to wait for; waiting for the RDS mixer only before the pre stages measured the
     // same, profiles/r04/release/)
     if (const int rw = release_wait(c, p, REL_MONO | REL_STEREO | REL_RDS, S(stream))) return rw;
-    const int r = frontend_launch(frontend_args(c, iq, iq_stride, p), S(stream));
+    FrontendArgs a = frontend_args(c, iq, iq_stride, p);
+    const bool timed = c->fe_time_n < c->fe_time_cap;
+    if (timed && c->fe_use_stamps) {   // sdr_frontend_timing: the kernel's own workgroup stamps
+        a.stamps = c->fe_stamps + (size_t)c->fe_time_n * c->fe_stamp_wgs * 2;
+    } else if (timed) {                // (other front ends) HIP events recorded with the launch
+        a.ev0 = c->fe_ev[2 * c->fe_time_n];
+        a.ev1 = c->fe_ev[2 * c->fe_time_n + 1];
+    }
+    const int r = frontend_launch(a, S(stream));
     if (r) return r;
+    if (timed) c->fe_time_n++;
     c->parity = p;
     c->block++;
+    return SDR_OK;
+}
+
+int sdr_frontend_timing(sdr_ctx* c, int max_launches) {
+    if (!c || max_launches < 0) return fail(SDR_E_INVALID, "frontend_timing: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const sdr_info& in = c->info;
+    c->fe_use_stamps = !(c->flags & SDR_FLAG_FAST_FRONTEND) && c->ntaps == 101 &&
+                       (in.rf_decim == 10 || in.rf_decim == 4 || in.rf_decim == 3);
+    if (c->fe_use_stamps) {
+        const int wgs = frontend_tiles(in.block_if) * c->nch;
+        if (c->fe_stamp_cap < max_launches || c->fe_stamp_wgs != wgs) {
+            if (c->fe_stamps) {
+                HIP_TRY(hipDeviceSynchronize());   // a pending timed launch may still write the old buffer
+                HIP_TRY(hipFree(c->fe_stamps));
+                c->fe_stamps = nullptr;
+            }
+            void* p = nullptr;
+            HIP_TRY(hipMalloc(&p, (size_t)std::max(max_launches, 1) * wgs * 2 * sizeof(unsigned long long)));
+            c->fe_stamps = static_cast<unsigned long long*>(p);
+            c->fe_stamp_cap = max_launches;
+            c->fe_stamp_wgs = wgs;
+        }
+    } else {
+        while ((int)c->fe_ev.size() < 2 * max_launches) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(hipEventCreate(&e));
+            c->fe_ev.push_back(e);
+        }
+    }
+    c->fe_time_cap = max_launches;
+    c->fe_time_n = 0;
+    return SDR_OK;
+}
+
+int sdr_frontend_times(sdr_ctx* c, double* ms, int max, int* n) {
+    if (!c || (!ms && max > 0)) return fail(SDR_E_INVALID, "frontend_times: bad arguments");
+    const int k = std::min(c->fe_time_n, std::max(max, 0));
+    if (c->fe_use_stamps) {
+        // each launch: the earliest workgroup start to the latest workgroup end (100 MHz ticks)
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipDeviceSynchronize());
+        const size_t per = (size_t)c->fe_stamp_wgs * 2;
+        std::vector<unsigned long long> h(per);
+        for (int i = 0; i < k; i++) {
+            HIP_TRY(hipMemcpy(h.data(), c->fe_stamps + (size_t)i * per, per * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost));
+            unsigned long long lo = ~0ull, hi = 0;
+            for (size_t g = 0; g < per; g += 2) {
+                lo = std::min(lo, h[g]);
+                hi = std::max(hi, h[g + 1]);
+            }
+            ms[i] = hi >= lo ? (double)(hi - lo) * 1e-5 : -1.0;
+        }
+    } else {
+        if (k > 0) HIP_TRY(hipEventSynchronize(c->fe_ev[2 * c->fe_time_n - 1]));
+        for (int i = 0; i < k; i++) {
+            float t = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&t, c->fe_ev[2 * i], c->fe_ev[2 * i + 1]));
+            ms[i] = t;
+        }
+    }
+    if (n) *n = k;
     return SDR_OK;
 }
 
@@ -2555,7 +2695,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         return fail(SDR_E_INVALID, "rds_post: resampler tile does not fit (L = %d)", c->rdsbb_L);
     dim3 gr(cdiv(in.n_rds, RLC_TN), cdiv(c->nch, 64));
     auto kr = c->rdsbb_all101 ? k_resample_lc<101> : k_resample_lc<0>;
-    hipLaunchKernelGGL(kr, gr, dim3(BLK), resample_lc_lds_bytes(c->rdsbb_L, 247, 640), s, rdc,
+    hipLaunchKernelGGL(kr, gr, dim3(BLK), resample_lc_lds_bytes(c->rdsbb_L, 247, 640, !c->rdsbb_all101), s, rdc,
                        c->fm_stride, -HIST, c->rdsbb_pp, c->rdsbb_cnt, c->rdsbb_L, c->rds_ptq, in.n_rds, c->nch,
                        rfilt, c->rf_stride);
     LAUNCH_CHECK();

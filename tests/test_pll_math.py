@@ -34,3 +34,19 @@ def test_dd_fallbacks_match_glibc(tmp_path):
     # |t| >= 2^30 (Payne-Hanek in double-double): the PLL's phase passes 2^30 after ~25 min (RDS)
     assert res["large"]["f32_mismatch"] == 0
     assert res["large"]["f64_mismatch"] < 0.005 * 2 * res["large"]["n"]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_nco_fast_cosine_matches_glibc(tmp_path):
+    """The NCO output RN_f32(cos(t * ncoScale + phaseAdjust)) (pll.cpp:52) of the fused post stages
+    (k_stereo_out, k_rds_mix) and k_nco_out: pll_math.h cos_rn_f32 (the PLL step's reduction and
+    kernels, one kernel selected by the quadrant, one tie proof) must equal glibc's f64 cos rounded to
+    f32 on every value it accepts -- near multiples of pi/2 and the stereo / RDS NCO arguments
+    included (tools/pllmath/validate_nco.cpp)."""
+    exe = tmp_path / "validate_nco"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", str(ROOT / "real-time-sdr_amd/csrc"),
+                    str(ROOT / "tools/pllmath/validate_nco.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "4000000"], capture_output=True, text=True, timeout=120)
+    res = json.loads(r.stdout)
+    assert r.returncode == 0 and res["f32_mismatch"] == 0, (res, r.stderr[-500:])
+    assert res["fallback"] < 1e-4 * res["n"]
