@@ -434,6 +434,9 @@ class GpuStepper:
                             "device_phase_ms": round(phase, 4), "fill_ms": round(phase - span - drain, 4),
                             "fill_parts": self.fill_parts if self.parts_block == first else 1,
                             "drain_ms": round(drain, 4)}
+                sides = self._fe_vs_pll(ts, te)
+                if sides:
+                    timeline["front_end_vs_pll_us"] = sides
         else:
             pll_ms = float(np.mean([self.pll_start[b].elapsed_time(self.pll_done[b]) for b in rng]))
         achieved = fe_bytes / fe_avg_s / 1e9
@@ -460,6 +463,31 @@ class GpuStepper:
                     **({"chunk_redo": redo} if redo else {}),
                     **({"waves": waves} if waves else {})},
         }
+
+    def _fe_vs_pll(self, ts: list, te: list) -> dict | None:
+        """Where each timed block's front end sat against the PLL (the same 100 MHz device clock:
+        the front end's own workgroup stamps, the persistent launch's per-block stamps), medians over
+        the phase's blocks j >= 2 (phase-relative; block 0 ran its front end in parts, untimed):
+          release_to_fe: front-end start - PLL end of block j-2 (its parity's readers run after it),
+          fe: the front end's span, fe_to_pll: PLL start of block j - front-end end (the pre-PLL FIRs
+          and the signal; when the PLL waited for the block), pll_gap: PLL start of j - PLL end of j-1."""
+        try:
+            f0, f1 = self.pipe.frontend_stamps()
+        except self.pkg.SdrError:
+            return None
+        off = 1 if self.parts_block == self.phase[0] else 0     # launch i = phase block i + off
+        rows = {"release_to_fe": [], "fe": [], "fe_to_pll": [], "pll_gap": []}
+        for i in range(len(f0)):
+            j = i + off
+            if j < 2 or j >= len(ts):
+                continue
+            rows["release_to_fe"].append((f0[i] - te[j - 2]) * 1e-2)
+            rows["fe"].append((f1[i] - f0[i]) * 1e-2)
+            rows["fe_to_pll"].append((ts[j] - f1[i]) * 1e-2)
+            rows["pll_gap"].append((ts[j] - te[j - 1]) * 1e-2)
+        if not rows["fe"]:
+            return None
+        return {k: round(float(np.median(v)), 1) for k, v in rows.items()}
 
     @staticmethod
     def _pll_issue(cyc) -> dict:

@@ -147,6 +147,9 @@ int sdr_frontend_release_wait(sdr_ctx *ctx, void *stream);
  * sdr_frontend_pre_parts launches are not timed. */
 int sdr_frontend_timing(sdr_ctx *ctx, int max_launches);
 int sdr_frontend_times(sdr_ctx *ctx, double *ms, int max, int *n);
+/* The same launches' earliest workgroup start and latest end as raw 100 MHz device ticks (the clock
+ * of sdr_plls_timeline), exact front end only: where each block's front end sat in the pipeline. */
+int sdr_frontend_stamps(sdr_ctx *ctx, unsigned long long *t_start, unsigned long long *t_end, int max, int *n);
 /* mono loop body (mono.cpp:34-42) on the current block: audio [nch][n_audio] int16 */
 int sdr_mono(sdr_ctx *ctx, int16_t *audio, size_t audio_stride, void *stream);
 /* stereo loop body (stereo.cpp:74-107): lr [nch][2*n_audio] int16, L/R interleaved */

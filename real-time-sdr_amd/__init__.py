@@ -84,6 +84,7 @@ def lib() -> C.CDLL:
         "sdr_frontend_release_wait": ([vp, vp], i32),
         "sdr_frontend_timing": ([vp, i32], i32),
         "sdr_frontend_times": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32)], i32),
+        "sdr_frontend_stamps": ([vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), i32, C.POINTER(i32)], i32),
         "sdr_mono": ([vp, vp, sz, vp], i32),
         "sdr_stereo": ([vp, vp, sz, vp], i32),
         "sdr_rds_dsp": ([vp, vp, sz, vp], i32),
@@ -302,6 +303,13 @@ class Pipeline:
         n = C.c_int(0)
         check(lib().sdr_frontend_times(self._h, arr, max_launches, C.byref(n)), "sdr_frontend_times")
         return list(arr[:n.value])
+
+    def frontend_stamps(self, max_launches: int = 4096) -> tuple[list, list]:
+        """(start, end) of each timed frontend() kernel in 100 MHz device ticks (plls_timeline's clock)."""
+        a, z = (C.c_ulonglong * max_launches)(), (C.c_ulonglong * max_launches)()
+        n = C.c_int(0)
+        check(lib().sdr_frontend_stamps(self._h, a, z, max_launches, C.byref(n)), "sdr_frontend_stamps")
+        return list(a[:n.value]), list(z[:n.value])
 
     def fm_demod(self, out=None, stream=None):
         import torch

@@ -2010,25 +2010,43 @@ int sdr_frontend_timing(sdr_ctx* c, int max_launches) {
     return SDR_OK;
 }
 
+// the timed launches' earliest workgroup start and latest workgroup end (100 MHz ticks)
+static int frontend_spans(sdr_ctx* c, int k, unsigned long long* t0, unsigned long long* t1) {
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    const size_t per = (size_t)c->fe_stamp_wgs * 2;
+    std::vector<unsigned long long> h(per);
+    for (int i = 0; i < k; i++) {
+        HIP_TRY(hipMemcpy(h.data(), c->fe_stamps + (size_t)i * per, per * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost));
+        unsigned long long lo = ~0ull, hi = 0;
+        for (size_t g = 0; g < per; g += 2) {
+            lo = std::min(lo, h[g]);
+            hi = std::max(hi, h[g + 1]);
+        }
+        t0[i] = lo;
+        t1[i] = hi;
+    }
+    return SDR_OK;
+}
+
+int sdr_frontend_stamps(sdr_ctx* c, unsigned long long* t_start, unsigned long long* t_end, int max, int* n) {
+    if (!c || !t_start || !t_end || max < 0) return fail(SDR_E_INVALID, "frontend_stamps: bad arguments");
+    if (!c->fe_use_stamps) return fail(SDR_E_INVALID, "frontend_stamps: only the exact front end stamps itself");
+    const int k = std::min(c->fe_time_n, max);
+    if (const int r = frontend_spans(c, k, t_start, t_end)) return r;
+    if (n) *n = k;
+    return SDR_OK;
+}
+
 int sdr_frontend_times(sdr_ctx* c, double* ms, int max, int* n) {
     if (!c || (!ms && max > 0)) return fail(SDR_E_INVALID, "frontend_times: bad arguments");
     const int k = std::min(c->fe_time_n, std::max(max, 0));
     if (c->fe_use_stamps) {
-        // each launch: the earliest workgroup start to the latest workgroup end (100 MHz ticks)
-        HIP_TRY(hipSetDevice(c->device));
-        HIP_TRY(hipDeviceSynchronize());
-        const size_t per = (size_t)c->fe_stamp_wgs * 2;
-        std::vector<unsigned long long> h(per);
-        for (int i = 0; i < k; i++) {
-            HIP_TRY(hipMemcpy(h.data(), c->fe_stamps + (size_t)i * per, per * sizeof(unsigned long long),
-                              hipMemcpyDeviceToHost));
-            unsigned long long lo = ~0ull, hi = 0;
-            for (size_t g = 0; g < per; g += 2) {
-                lo = std::min(lo, h[g]);
-                hi = std::max(hi, h[g + 1]);
-            }
-            ms[i] = hi >= lo ? (double)(hi - lo) * 1e-5 : -1.0;
-        }
+        // each launch: the earliest workgroup start to the latest workgroup end
+        std::vector<unsigned long long> t0((size_t)std::max(k, 1)), t1((size_t)std::max(k, 1));
+        if (const int r = frontend_spans(c, k, t0.data(), t1.data())) return r;
+        for (int i = 0; i < k; i++) ms[i] = t1[i] >= t0[i] ? (double)(t1[i] - t0[i]) * 1e-5 : -1.0;
     } else {
         if (k > 0) HIP_TRY(hipEventSynchronize(c->fe_ev[2 * c->fe_time_n - 1]));
         for (int i = 0; i < k; i++) {

@@ -531,6 +531,8 @@ __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx
     const double u = pllm::fma_(rr, L.k1, L.k0);
     // Horner: one instruction fewer than Estrin (no z^2), two dependent levels more; faster than
     // Estrin and than a two-level form (profiles/r03/ab_pll_split3.txt)
+    // (Estrin, two dependent levels shorter for two multiplies more, measured again in round 5:
+    // 212 -> 224 cycles per step, with or without s_setprio; profiles/r05/ab_pll_est.txt)
     double P = pllm::fma_(z, L.c5, L.c4);
     P = pllm::fma_(z, P, L.c3);
     P = pllm::fma_(z, P, L.c2);
