@@ -181,10 +181,14 @@ PLLM_HD Phase phase_detect(float eI, float eQ, double c, double s, double mr, in
 //    2^-66). d = Y * rx replaces Y / X with an absolute error <= |d| (|delta| + 2^-51) < 2^-45.9,
 //    and atan2(eQ, eI) = base + d where base = -t + pi [x < 0] (mod 2pi) is prepared from the
 //    PREVIOUS step's quadrant before this step's input is touched (base_angle). EPS_ABS_E2 bounds
-//    the total absolute error (d, the reduction, base, the final add).
+//    the distance from e to the reference's f64 atan2: d's 2^-45.9, the kernels' 0.5 (eps_s +
+//    eps_c) < 2^-48.3, base's and the final add's roundings (2^-52 each), the representation of
+//    pi/2 times |m| <= 2 (2^-52.8), glibc atan2's own <= 1 ulp (2^-51): 2^-45.56 in all, under
+//    2^-45 (round 5; 2^-44 before, profiles/r05/: half the chunk redos). Measured:
+//    tools/pllmath/validate_e2.cpp, 2^-47.9 over 2e7 samples.
 // ------------------------------------------------------------------------------------------
 constexpr double MAGIC = 6755399441055744.0;   // 1.5 * 2^52: fma(x, c, MAGIC) - MAGIC = rint(x c)
-constexpr double EPS_ABS_E2 = 0x1p-44;
+constexpr double EPS_ABS_E2 = 0x1p-45;
 
 PLLM_HD double pll_rx(float x) {
     const float ax = __builtin_fabs(x);

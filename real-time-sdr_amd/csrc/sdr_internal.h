@@ -132,6 +132,7 @@ int launch_flag_store(uint32_t* flag, uint32_t v, hipStream_t s);
 int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStream_t s);
 int diag_pll_counts(unsigned long long* out, int reset);
 int diag_pll_waves(unsigned long long* out, int nmax);
+int diag_pll_hwid(unsigned long long* out, int nmax);
 constexpr int PLL_WORDS_DONE = 4;      // index of the done ring in the words array
 // words[PLL_WORD_SUB]: the parts of a launch's first block published so far, as launch_base *
 // PLL_SUB_SCALE + FIR tiles (a value no earlier launch can have left behind: no reset needed)

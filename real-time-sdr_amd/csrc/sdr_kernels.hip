@@ -1661,6 +1661,8 @@ extern "C" int sdr_diag_hold(void* stream, int ms) {
 extern "C" int sdr_diag_pll_counts(unsigned long long* out, int reset) { return diag_pll_counts(out, reset); }
 // Diagnosis builds only (-DSDR_PLL_WAVES=1): per-wave totals of the last persistent launch; -1 otherwise.
 extern "C" int sdr_diag_pll_waves(unsigned long long* out, int nmax) { return diag_pll_waves(out, nmax); }
+// Diagnosis builds only (-DSDR_PLL_HWID=1): placement and duration of the last k_pll launch's waves.
+extern "C" int sdr_diag_pll_hwid(unsigned long long* out, int nmax) { return diag_pll_hwid(out, nmax); }
 
 int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int flags) {
     if (!out || nch <= 0) return fail(SDR_E_INVALID, "bad arguments");

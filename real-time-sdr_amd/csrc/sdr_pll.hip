@@ -145,6 +145,17 @@ __device__ unsigned long long g_flag_t[64];
 __device__ const uint32_t* g_diag_flag;
 #endif
 
+#ifndef SDR_PLL_HWID
+#define SDR_PLL_HWID 0    // diagnosis build: where each k_pll wave ran and for how long (sdr_diag_pll_hwid)
+#endif
+#if SDR_PLL_HWID
+// per wave of the last k_pll launches (slot = blockIdx.y * gridDim.x + blockIdx.x): [0] HW_ID
+// (wave slot, SIMD, CU, shader array, SE), [1] XCC_ID, [2] shader cycles from entry to exit, [3], [4]
+// 100 MHz time at entry and at exit
+constexpr int PLL_HWID_SLOTS = 4096, PLL_HWID_FIELDS = 5;
+__device__ unsigned long long g_pll_hwid[PLL_HWID_SLOTS][PLL_HWID_FIELDS];
+#endif
+
 // TAB: the trigArg offsets come from a table whose range the kernel checked once (pll_run)
 template <bool TAB>
 __device__ __forceinline__ bool pll_chunk_ok(const PllProof& pf, const PllRegs& r, double w, int chunk) {
@@ -756,6 +767,9 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
         __syncthreads();
     }
     if (!active) return;
+#if SDR_PLL_HWID
+    const unsigned long long hw_c0 = __builtin_amdgcn_s_memtime(), hw_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (SPLIT) {
         if (tab) pll_run_split<VEC, true>(jb, n, ch, wtab);
         else pll_run_split<VEC, false>(jb, n, ch, nullptr);
@@ -763,6 +777,20 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
         if (tab) pll_run<VEC, true>(jb, n, ch, wtab);
         else pll_run<VEC, false>(jb, n, ch, nullptr);
     }
+#if SDR_PLL_HWID
+    const unsigned long long hw_c1 = __builtin_amdgcn_s_memtime(), hw_r1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t hw_id, xcc_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
+    const int slot = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    if (threadIdx.x == 0 && slot < PLL_HWID_SLOTS) {
+        g_pll_hwid[slot][0] = hw_id;
+        g_pll_hwid[slot][1] = xcc_id;
+        g_pll_hwid[slot][2] = hw_c1 - hw_c0;
+        g_pll_hwid[slot][3] = hw_r0;
+        g_pll_hwid[slot][4] = hw_r1;
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1181,6 +1209,21 @@ int diag_pll_waves(unsigned long long* out, int nmax) {
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pll_waves), sizeof(unsigned long long) * PLL_WAVE_FIELDS * nw));
     static unsigned long long z[PLL_WAVE_SLOTS][PLL_WAVE_FIELDS];
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pll_waves), z, sizeof z));
+    return nw;
+#else
+    (void)out;
+    (void)nmax;
+    return -1;
+#endif
+}
+
+// Diagnosis builds only (-DSDR_PLL_HWID=1): placement and duration of the last k_pll launch's waves
+// (g_pll_hwid), at most nmax waves of PLL_HWID_FIELDS (5) values; -1 in product builds.
+int diag_pll_hwid(unsigned long long* out, int nmax) {
+#if SDR_PLL_HWID
+    const int nw = std::min(nmax, PLL_HWID_SLOTS);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pll_hwid), sizeof(unsigned long long) * PLL_HWID_FIELDS * nw));
     return nw;
 #else
     (void)out;

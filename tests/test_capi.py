@@ -45,6 +45,9 @@ def test_diagnosis_counters_absent_in_product_build(pkg):
     # the per-wave totals of -DSDR_PLL_WAVES=1 builds (bench.py pll.waves) likewise
     waves = (C.c_ulonglong * (8 * 4))()
     assert pkg.lib().sdr_diag_pll_waves(waves, 4) == -1
+    # and the wave placement of -DSDR_PLL_HWID=1 builds (tools/diag_pll_place.py)
+    hwid = (C.c_ulonglong * (5 * 4))()
+    assert pkg.lib().sdr_diag_pll_hwid(hwid, 4) == -1
 
 
 def test_product_taps_equal_reference_taps(pkg, golden):

@@ -50,3 +50,19 @@ def test_nco_fast_cosine_matches_glibc(tmp_path):
     res = json.loads(r.stdout)
     assert r.returncode == 0 and res["f32_mismatch"] == 0, (res, r.stderr[-500:])
     assert res["fallback"] < 1e-4 * res["n"]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_phase_detector_error_inside_e_bracket(tmp_path):
+    """The e bracket EPS_ABS_E2 = 2^-45 (pll_math.h: analytic bound 2^-45.56 on |e - glibc atan2|)
+    against the measured error: e of sincos2_f32 + base_angle + phase_detect2 and glibc's f64 atan2,
+    each against a 64-bit-mantissa atan2l (tools/pllmath/validate_e2.cpp). The measured sum must stay
+    well inside the bracket (2^-47.8 at 2e7 samples)."""
+    exe = tmp_path / "validate_e2"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", str(ROOT / "real-time-sdr_amd/csrc"),
+                    str(ROOT / "tools/pllmath/validate_e2.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, timeout=120)
+    res = json.loads(r.stdout)
+    assert r.returncode == 0 and res["n"] > 1_900_000, res
+    assert res["log2_eps"] == -45.0
+    assert res["log2_sum"] < res["log2_eps"] - 1.5, res

@@ -9,9 +9,11 @@
 // instruction for 1, 2 and 4 waves per CU: one workgroup per CU (96 KiB of dynamic LDS each) of 64,
 // 128 or 256 threads, whose waves the dispatcher puts on distinct SIMDs.
 //   hipcc --offload-arch=gfx950 -O3 tools/microbench/ifetch.hip -o tools/microbench/bin/ifetch
+//   tools/microbench/bin/ifetch wg1    (one-wave workgroups with the PLL's register footprint, k_fma1)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <string>
 #include <vector>
 
 #define CHECK(x)                                                                        \
@@ -124,7 +126,82 @@ int run(const char* name, int per_cu, int ncu, double* out, unsigned long long* 
     return 0;
 }
 
-int main() {
+// One-wave workgroups, per_cu of them per CU (grid = per_cu * ncu), with the PLL's register
+// footprint (v255 and AGPRs in use: one wave per SIMD, as k_pll's 256 VGPRs + 18 AGPRs): the k_pll
+// launch shape of DESIGN.md 5's four-waves-per-CU case, on independent f64 fma chains. Each wave
+// records its HW_ID and XCC_ID beside its cycles, so placement and slowdown can be put side by side.
+template <int OP>
+__global__ __launch_bounds__(64) void k_fma1(double* out, unsigned long long* rec, int outer, double b, double c) {
+    asm volatile("" ::: "v255", "a31");
+    double a[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = threadIdx.x + k;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int o = 0; o < outer; o++) {
+#pragma unroll
+        for (int u = 0; u < 256; u++) {
+            if (OP == 0) a[u & 7] = __builtin_fma(a[u & 7], b, c);
+            else asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a[0]) : "v"(b), "v"(c));
+        }
+        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
+                     "+v"(a[7]));
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) s += a[k];
+    if (s == 12345.678) out[threadIdx.x] = s;
+    if (threadIdx.x == 0) {
+        rec[3 * blockIdx.x] = t1 - t0;
+        rec[3 * blockIdx.x + 1] = hw;
+        rec[3 * blockIdx.x + 2] = xcc;
+    }
+}
+
+template <int OP>
+int run1(int per_cu, int ncu, double* out, unsigned long long* rec) {
+    const long NI = 1 << 21;
+    const int outer = (int)(NI / 256);
+    const int grid = per_cu * ncu;
+    for (int rep = 0; rep < 2; rep++) {
+        hipLaunchKernelGGL(k_fma1<OP>, dim3(grid), dim3(64), 0, 0, out, rec, outer, 1.0000001, 1e-9);
+        CHECK(hipDeviceSynchronize());
+    }
+    std::vector<unsigned long long> h(3 * grid);
+    CHECK(hipMemcpy(h.data(), rec, 3 * grid * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    // waves per (xcc, se, sh, cu) and per SIMD; cycles per instruction by how many waves shared the SIMD
+    std::vector<int> cu_n(16 * 8 * 2 * 16, 0), simd_n(16 * 8 * 2 * 16 * 4, 0);
+    auto cu_key = [&](int g) {
+        const unsigned hw = (unsigned)h[3 * g + 1], x = (unsigned)h[3 * g + 2] & 15u;
+        return (int)(((x * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15));
+    };
+    for (int g = 0; g < grid; g++) {
+        cu_n[cu_key(g)]++;
+        simd_n[cu_key(g) * 4 + (((unsigned)h[3 * g + 1] >> 4) & 3)]++;
+    }
+    double sum[5] = {}, cnt[5] = {};
+    int cus = 0, shared_simds = 0, maxcu = 0;
+    for (int v : cu_n) { cus += v > 0; maxcu = v > maxcu ? v : maxcu; }
+    for (int v : simd_n) shared_simds += v > 1;
+    for (int g = 0; g < grid; g++) {
+        const int k = std::min(simd_n[cu_key(g) * 4 + (((unsigned)h[3 * g + 1] >> 4) & 3)], 4);
+        sum[k] += (double)h[3 * g];
+        cnt[k] += 1.0;
+    }
+    std::printf("{\"kernel\": \"one-wave workgroups, 1 wave/SIMD footprint\", \"op\": \"%s\", \"waves_per_cu\": %d, "
+                "\"cus_used\": %d, \"max_waves_on_a_cu\": %d, \"simds_with_2plus_waves\": %d",
+                OP == 0 ? "v_fma_f64, 8 chains" : "v_fma_f64, one dependent chain", per_cu, cus, maxcu, shared_simds);
+    for (int k = 1; k <= 4; k++)
+        if (cnt[k] > 0)
+            std::printf(", \"cpi_waves_on_simd_%d\": %.3f", k, sum[k] / cnt[k] / (double)NI);
+    std::printf("}\n");
+    return 0;
+}
+
+int main(int argc, char** argv) {
     int ncu = 0;
     CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     double* out = nullptr;
@@ -132,6 +209,15 @@ int main() {
     CHECK(hipMalloc(&out, 4096 * sizeof(double)));
     CHECK(hipMemset(out, 0, 4096 * sizeof(double)));
     CHECK(hipMalloc(&cyc, 4 * 1024 * sizeof(unsigned long long)));
+    if (argc > 1 && std::string(argv[1]) == "wg1") {   // one-wave workgroups (k_fma1)
+        unsigned long long* rec = nullptr;
+        CHECK(hipMalloc(&rec, 3 * 8 * (size_t)ncu * sizeof(unsigned long long)));
+        for (int per_cu : {1, 2, 4, 5, 8}) {
+            if (run1<0>(per_cu, ncu, out, rec)) return 1;
+            if (run1<1>(per_cu, ncu, out, rec)) return 1;
+        }
+        return 0;
+    }
     for (int per_cu : {1, 4}) {
         if (run<2048, 0>("straight", per_cu, ncu, out, cyc)) return 1;
         if (run<64, 0>("tight", per_cu, ncu, out, cyc)) return 1;
