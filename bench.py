@@ -556,7 +556,10 @@ class GpuStepper:
 
     def isolated_frontend(self) -> dict:
         """Outside the timed region: the front-end kernel of both numerics modes alone on the GPU
-        (one stream, the same resident inputs), each as a roofline object."""
+        (one stream, the same resident inputs, 20 back-to-back launches), each as a roofline object
+        whose launch time is the kernel's own (its workgroups' start / end stamps, sdr_frontend_times,
+        as in the pipeline line); avg_call_ms_events: HIP events around the 20 calls, per call
+        (kernel plus the gap between dependent dispatches)."""
         torch, pkg, nch, info = self.torch, self.pkg, self.nch, self.info
         fe_bytes = nch * (2 * info.block_iq + 4 * info.block_if)
         res = {}
@@ -567,17 +570,22 @@ class GpuStepper:
                 p2.frontend(self.iq[b], stream=s2)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             reps = 20
+            p2.frontend_timing(reps)
             e0.record(s2)
             for b in range(reps):
                 p2.frontend(self.iq[b % self.nblocks], stream=s2)
             e1.record(s2)
             torch.cuda.synchronize(self.dev)
-            ms = e0.elapsed_time(e1) / reps
+            ms_calls = e0.elapsed_time(e1) / reps
+            kern = p2.frontend_times(reps)
+            ms = float(np.mean(kern)) if kern else ms_calls
             gbs = fe_bytes / (ms / 1e3) / 1e9
             res[name] = {"kernel": "k_frontend_mfma (int8 MFMA Toeplitz FIR)" if flags else "k_frontend2",
                          "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(nch, name),
-                         "avg_launch_ms": round(ms, 4)}
+                         "avg_launch_ms": round(ms, 4), "launches_timed": len(kern),
+                         "timed_by": "the kernel's own workgroup start/end stamps" if kern else "HIP events",
+                         "avg_call_ms_events": round(ms_calls, 4)}
             if not flags:
                 # exact mode is VALU-bound (f32 multiply and add per tap, no FMA): the same time
                 # against the f32 vector peak (report the VALU fraction too)

@@ -140,15 +140,15 @@ int sdr_frontend(sdr_ctx *ctx, const uint8_t *iq, size_t iq_stride, void *stream
  * kernel alone. Optional. */
 int sdr_frontend_release_wait(sdr_ctx *ctx, void *stream);
 /* Kernel timing of the front end (no reference counterpart; for benchmarks): the next `max_launches`
- * sdr_frontend kernels are timed -- the exact front end by its own workgroups' start and end stamps
- * (s_memrealtime: the earliest start to the latest end, the kernel's span as a rocprofv3 kernel
- * trace sees it), the others by HIP events recorded with the launch -- and sdr_frontend_times
- * returns them in ms (synchronising the device). 0 disables; each call re-arms from the first.
- * sdr_frontend_pre_parts launches are not timed. */
+ * sdr_frontend kernels are timed -- the 101-tap exact and fast (MFMA) front ends by their own
+ * workgroups' start and end stamps (s_memrealtime: the earliest start to the latest end, the kernel's
+ * span as a rocprofv3 kernel trace sees it), the generic one by HIP events recorded with the launch
+ * -- and sdr_frontend_times returns them in ms (synchronising the device). 0 disables; each call
+ * re-arms from the first. sdr_frontend_pre_parts launches are not timed. */
 int sdr_frontend_timing(sdr_ctx *ctx, int max_launches);
 int sdr_frontend_times(sdr_ctx *ctx, double *ms, int max, int *n);
 /* The same launches' earliest workgroup start and latest end as raw 100 MHz device ticks (the clock
- * of sdr_plls_timeline), exact front end only: where each block's front end sat in the pipeline. */
+ * of sdr_plls_timeline), stamping front ends only: where each block's front end sat in the pipeline. */
 int sdr_frontend_stamps(sdr_ctx *ctx, unsigned long long *t_start, unsigned long long *t_end, int max, int *n);
 /* mono loop body (mono.cpp:34-42) on the current block: audio [nch][n_audio] int16 */
 int sdr_mono(sdr_ctx *ctx, int16_t *audio, size_t audio_stride, void *stream);

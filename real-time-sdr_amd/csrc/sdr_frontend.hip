@@ -249,8 +249,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
     const v4i* __restrict__ afrag, double yscale, int block_iq, int block_if,
     float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int tiles_ch,
-    const uint32_t* __restrict__ pad) {
+    const uint32_t* __restrict__ pad, unsigned long long* __restrict__ stamps) {
     static_assert(15 * D + 101 <= 256, "one block's window must fit K = 256");
+    // sdr_frontend_timing: this workgroup's start and end on the 100 MHz clock (as k_frontend2)
+    if (stamps && threadIdx.x == 0) stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     static_assert(NB % 8 == 0, "whole C tiles");
     constexpr int HP = 100, WIN = ft_win(D, NB), G = WIN / 8;
     constexpr int ADV = ft_adv(D, NB), CARRY = ft_carry(D);
@@ -323,6 +325,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         for (int i = t; i < HP; i += 64) tout[i] = last[i];
         const float* o = fm_other + (size_t)ch * fm_stride;
         for (int i = t; i < HIST; i += 64) out[i - HIST] = o[block_if - HIST + i];
+    }
+    if (stamps) {   // the end: after this wave's stores have completed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -529,9 +535,10 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0, int jn) {
     if (jn <= 0) { j0 = 0; jn = tiles_ch; }
     if (j0 < 0 || j0 + jn > tiles_ch) return fail(SDR_E_INVALID, "frontend: tiles [%d, %d) of %d", j0, j0 + jn, tiles_ch);
     const dim3 g2(jn * a.nch);
-    // sdr_frontend_timing: k_frontend2 stamps each workgroup's start and end (a.stamps); the other
-    // front ends record HIP events with the launch (hipExtLaunchKernelGGL: the start event is a marker
-    // ahead of the dispatch, so its span exceeds the kernel's by the marker's latency, ~9 us)
+    // sdr_frontend_timing: k_frontend2 and k_frontend_mfma stamp each workgroup's start and end
+    // (a.stamps); the generic kernel records HIP events with the launch (hipExtLaunchKernelGGL: the
+    // start event is a marker ahead of the dispatch, so its span exceeds the kernel's by the marker's
+    // latency, ~9 us)
 #define FE2(DD)                                                                                               \
     hipExtLaunchKernelGGL((k_frontend2<FE_R, DD>), g2, dim3(64), 0, s, a.ev0, a.ev1, 0, iq, iq_stride, tail_in, \
                           tail_out, prev_in, prev_out, a.hs, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride, j0, jn, \
@@ -546,7 +553,7 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0, int jn) {
         hipExtLaunchKernelGGL((k_frontend_mfma<DD, XX, NB>), dim3(cdiv(a.block_if, ft_adv(DD, NB)) * a.nch),   \
                               dim3(64), 0, s, a.ev0, a.ev1, 0, iq, iq_stride, tail_in, tail_out, prev_in, prev_out, af, \
                               a.yscale, a.block_iq, a.block_if, fm_p, fm_o, a.fm_stride,                            \
-                              cdiv(a.block_if, ft_adv(DD, NB)), a.pad80)
+                              cdiv(a.block_if, ft_adv(DD, NB)), a.pad80, a.stamps)
         if (a.D == 10) { if (x4) FEM(10, true); else FEM(10, false); }
         else if (a.D == 4) { if (x4) FEM(4, true); else FEM(4, false); }
         else { if (x4) FEM(3, true); else FEM(3, false); }
@@ -569,6 +576,12 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0, int jn) {
 #undef FE2
     LAUNCH_CHECK();
     return SDR_OK;
+}
+
+int frontend_stamp_wgs(int block_if, int nch, int ntaps, int D, bool fast) {
+    if (D != 10 && D != 4 && D != 3) return 0;
+    if (fast) return cdiv(block_if, ft_adv(D, FT_NB)) * nch;
+    return ntaps == 101 ? frontend_tiles(block_if) * nch : 0;
 }
 
 }  // namespace sdrk

@@ -110,6 +110,8 @@ struct FrontendArgs {
 int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0 = 0, int jn = 0);
 int frontend_tiles(int block_if);   // exact front-end tiles per channel and block
 int frontend_tab_r();               // outputs per lane of the exact front end (tap-table row length)
+// workgroups of a whole-block launch that stamps itself (sdr_frontend_timing), 0: the kernel does not
+int frontend_stamp_wgs(int block_if, int nch, int ntaps, int D, bool fast);
 
 // ---- sdr_pll.hip
 int launch_nco(const PllJobs& jobs, int njobs, int n, int nch, hipStream_t s);

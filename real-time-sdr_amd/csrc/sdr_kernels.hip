@@ -1984,10 +1984,9 @@ int sdr_frontend_timing(sdr_ctx* c, int max_launches) {
     if (!c || max_launches < 0) return fail(SDR_E_INVALID, "frontend_timing: bad arguments");
     HIP_TRY(hipSetDevice(c->device));
     const sdr_info& in = c->info;
-    c->fe_use_stamps = !(c->flags & SDR_FLAG_FAST_FRONTEND) && c->ntaps == 101 &&
-                       (in.rf_decim == 10 || in.rf_decim == 4 || in.rf_decim == 3);
+    const int wgs = frontend_stamp_wgs(in.block_if, c->nch, c->ntaps, in.rf_decim, c->flags & SDR_FLAG_FAST_FRONTEND);
+    c->fe_use_stamps = wgs > 0;
     if (c->fe_use_stamps) {
-        const int wgs = frontend_tiles(in.block_if) * c->nch;
         if (c->fe_stamp_cap < max_launches || c->fe_stamp_wgs != wgs) {
             if (c->fe_stamps) {
                 HIP_TRY(hipDeviceSynchronize());   // a pending timed launch may still write the old buffer
@@ -2034,7 +2033,7 @@ static int frontend_spans(sdr_ctx* c, int k, unsigned long long* t0, unsigned lo
 
 int sdr_frontend_stamps(sdr_ctx* c, unsigned long long* t_start, unsigned long long* t_end, int max, int* n) {
     if (!c || !t_start || !t_end || max < 0) return fail(SDR_E_INVALID, "frontend_stamps: bad arguments");
-    if (!c->fe_use_stamps) return fail(SDR_E_INVALID, "frontend_stamps: only the exact front end stamps itself");
+    if (!c->fe_use_stamps) return fail(SDR_E_INVALID, "frontend_stamps: only the 101-tap front ends stamp themselves");
     const int k = std::min(c->fe_time_n, max);
     if (const int r = frontend_spans(c, k, t_start, t_end)) return r;
     if (n) *n = k;

@@ -164,6 +164,43 @@ def test_fast_frontend_modes_vs_oracle(pkg, synth, oracle, torch_cuda, mode, row
             assert err <= 1e-5 * scale, f"mode {mode} ch {c} block {b}: {err / scale:.2e}"
 
 
+@pytest.mark.parametrize("fast", [False, True], ids=["exact", "fast_mfma"])
+@pytest.mark.parametrize("mode", [0, 1, 3])
+def test_frontend_timing_stamps(pkg, synth, torch_cuda, fast, mode):
+    """sdr_frontend_timing on the exact (k_frontend2) and MFMA (k_frontend_mfma) front ends: the
+    timed launches stamp their workgroups (bench.py's roofline launch time), report one positive span
+    per launch, in order and without overlap on one stream, and leave fm_demod bit-identical to
+    untimed launches on the same bytes (modes 0, 1, 3: D = 10, 4, 3)."""
+    import real_time_sdr_amd.synth as s
+    torch = torch_cuda
+    nch, nb = 40, 4
+    flags = pkg.FLAG_FAST_FRONTEND if fast else 0
+    p0 = pkg.Pipeline(1, mode=mode)
+    block_iq = p0.info.block_iq
+    p0.close()
+    srcs = [s.FMMultiplexSource(70 + c) for c in range(nch)]
+    host = np.stack([np.stack([src.next_block(block_iq) for src in srcs]) for _ in range(nb)])
+    iq = torch.from_numpy(host).cuda()
+    fms = []
+    for timed in (False, True):
+        pipe = pkg.Pipeline(nch, mode=mode, flags=flags)
+        if timed:
+            pipe.frontend_timing(nb)
+        got = []
+        for b in range(nb):
+            pipe.frontend(iq[b])
+            got.append(pipe.fm_demod().cpu().numpy())
+        if timed:
+            ms = pipe.frontend_times(nb)
+            t0, t1 = pipe.frontend_stamps(nb)
+            assert len(ms) == nb and all(0.0 < v < 50.0 for v in ms), ms
+            assert all(t1[i] <= t0[i + 1] for i in range(nb - 1)), (t0, t1)
+        fms.append(got)
+        pipe.close()
+    for b in range(nb):
+        assert np.array_equal(fms[0][b], fms[1][b]), f"block {b}: timing changed fm_demod"
+
+
 def test_reset_restarts_stream(pkg, synth, torch_cuda):
     iq = channel_input(synth, 0, 3)
     torch = torch_cuda
