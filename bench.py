@@ -224,9 +224,13 @@ class GpuStepper:
         self.pll_start, self.pll_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
         self.gather_done = [ev() for _ in range(nblocks)]
         self.pre_done, self.post_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
-        # SDR_BENCH_FE_WAIT=post: the front end of block b also waits for block b-2's whole post
-        # stream work (the output copies and captures included), as before the library's own release
-        self.fe_waits_post = os.environ.get("SDR_BENCH_FE_WAIT", "library") == "post"
+        # the front end of block b also waits for block b-2's whole post stream work (the RDS chain
+        # after its mixer, the output copies and captures included), not only for the library's own
+        # parity release (its readers' first kernels): the front end then runs beside the PLL alone
+        # instead of beside block b-2's RDS chain -- 0.111 against 0.140 ms per front end and 0.6954-
+        # 0.7088 against 0.7115-0.7189 ms per step, 3 interleaved pairs (profiles/r05/fe_wait_ab.txt).
+        # SDR_BENCH_FE_WAIT=library (A/B): the parity release alone.
+        self.fe_waits_post = os.environ.get("SDR_BENCH_FE_WAIT", "post") == "post"
         # outputs of a few channels, captured on the producing streams for the check after timing
         nv = min(VERIFY_CHANNELS, nch)
         self.vsel = torch.tensor(sorted({int(round(i * (nch - 1) / max(1, nv - 1))) for i in range(nv)}),
