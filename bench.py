@@ -230,7 +230,10 @@ class GpuStepper:
         # instead of beside block b-2's RDS chain -- 0.111 against 0.140 ms per front end and 0.6954-
         # 0.7088 against 0.7115-0.7189 ms per step, 3 interleaved pairs (profiles/r05/fe_wait_ab.txt).
         # SDR_BENCH_FE_WAIT=library (A/B): the parity release alone.
-        self.fe_waits_post = os.environ.get("SDR_BENCH_FE_WAIT", "post") == "post"
+        # Past 1024 channels per GPU the side chain, not the PLL, sets the period, and that wait
+        # lengthens its critical path (2048 channels: 143.0 against 148.7 GS/s), so there the
+        # release alone orders the front end.
+        self.fe_waits_post = os.environ.get("SDR_BENCH_FE_WAIT", "post" if nch <= 1024 else "library") == "post"
         # outputs of a few channels, captured on the producing streams for the check after timing
         nv = min(VERIFY_CHANNELS, nch)
         self.vsel = torch.tensor(sorted({int(round(i * (nch - 1) / max(1, nv - 1))) for i in range(nv)}),

@@ -467,7 +467,13 @@ __global__ __launch_bounds__(BLK) void k_resample(const float* __restrict__ xa, 
 // ptq[n] = (q << 8) | phase with phase = nD mod U, q = nD / U (host table; U < 256). Sums stay
 // in ascending j (= ascending k of the reference) as f32 product then f32 add.
 // ------------------------------------------------------------------------------------------
-constexpr int RLC_TN = 32;     // outputs per workgroup (8 per wave; 16: 218 VGPRs, 2 waves per SIMD)
+// outputs per workgroup, over 8 waves of 4 outputs: the x tile (64 channels x the tile's q span,
+// 46 KB of LDS) bounds a CU to 2-3 workgroups, so 8 waves per workgroup instead of 4 give 16 waves per
+// CU instead of 12 to hide the tap rows' scalar-load latency: 44.5 -> 37.7 us isolated. 16 outputs
+// per workgroup (4 waves) or the tap rows by vector loads (lc_group_v, in order, 2 chunks ahead)
+// were slower: 45.2, 59.5 us (profiles/r05/resample_lc_ab.txt).
+constexpr int RLC_TN = 32;
+constexpr int RLC_BLK = 64 * 8;   // threads per workgroup
 constexpr int RLC_XL = 3;      // staged samples per lane and row: 64 * 3 >= the q span + look-back
 constexpr int RLC_HL = 2;      // staged taps per lane and polyphase row: 64 * 2 >= L4
 
@@ -567,13 +573,13 @@ __device__ __forceinline__ void lc_group_s(const float* __restrict__ xr, const f
 }
 
 template <int NTAP>   // > 0: every polyphase row has exactly NTAP taps (fully unrolled sums)
-__global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x, size_t x_stride, int hist_lo,
+__global__ __launch_bounds__(RLC_BLK) void k_resample_lc(const float* __restrict__ x, size_t x_stride, int hist_lo,
                                                      const float* __restrict__ hp, const int* __restrict__ cnt,
                                                      int L, const int* __restrict__ ptq, int ny, int nch,
                                                      float* __restrict__ y, size_t y_stride) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
-    constexpr int PW = RLC_TN / (BLK / 64);                  // outputs per wave
+    constexpr int PW = RLC_TN / (RLC_BLK / 64);              // outputs per wave
     const int c0 = blockIdx.y * 64, n0 = blockIdx.x * RLC_TN;
     const int nn = min(RLC_TN, ny - n0);
     // wave index as a scalar: the per-output table reads (ptq, cnt) are then scalar loads issued
@@ -590,11 +596,11 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
     // staging with every load of a wave in flight before its LDS writes: rows c = wave + 4u of the
     // x tile (lanes along the row, RLC_XL loads per row), then the polyphase rows of the outputs
     {
-        constexpr int NR = 64 / (BLK / 64);
+        constexpr int NR = 64 / (RLC_BLK / 64);
         float v[NR][RLC_XL];
 #pragma unroll
         for (int u = 0; u < NR; u++) {
-            const int ch = min(c0 + wave + u * (BLK / 64), nch - 1);
+            const int ch = min(c0 + wave + u * (RLC_BLK / 64), nch - 1);
             const float* xc = x + (size_t)ch * x_stride;
 #pragma unroll
             for (int k = 0; k < RLC_XL; k++) {
@@ -620,7 +626,7 @@ __global__ __launch_bounds__(BLK) void k_resample_lc(const float* __restrict__ x
         }
 #pragma unroll
         for (int u = 0; u < NR; u++) {
-            const int c = wave + u * (BLK / 64);
+            const int c = wave + u * (RLC_BLK / 64);
 #pragma unroll
             for (int k = 0; k < RLC_XL; k++) {
                 const int i = lane + 64 * k;
@@ -874,8 +880,11 @@ struct StereoOut {
     Poison err;                 // the block's error words (persistent PLL launch, release timeout)
 };
 
+#ifndef SDR_STO_WPE
+#define SDR_STO_WPE 1
+#endif
 template <int D>
-__global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
+__global__ __launch_bounds__(AT) __attribute__((amdgpu_waves_per_eu(SDR_STO_WPE))) void k_stereo_out(const StereoOut a) {
     constexpr int WIN = audio_win<D>(), TW = audio_tw<D>();
     __shared__ __attribute__((aligned(16))) float sa[(WIN + 3) / 4 * 4 + 4];
     __shared__ __attribute__((aligned(16))) float sb[(WIN + 3) / 4 * 4 + 4];
@@ -2714,7 +2723,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         return fail(SDR_E_INVALID, "rds_post: resampler tile does not fit (L = %d)", c->rdsbb_L);
     dim3 gr(cdiv(in.n_rds, RLC_TN), cdiv(c->nch, 64));
     auto kr = c->rdsbb_all101 ? k_resample_lc<101> : k_resample_lc<0>;
-    hipLaunchKernelGGL(kr, gr, dim3(BLK), resample_lc_lds_bytes(c->rdsbb_L, 247, 640, !c->rdsbb_all101), s, rdc,
+    hipLaunchKernelGGL(kr, gr, dim3(RLC_BLK), resample_lc_lds_bytes(c->rdsbb_L, 247, 640, !c->rdsbb_all101), s, rdc,
                        c->fm_stride, -HIST, c->rdsbb_pp, c->rdsbb_cnt, c->rdsbb_L, c->rds_ptq, in.n_rds, c->nch,
                        rfilt, c->rf_stride);
     LAUNCH_CHECK();
