@@ -880,11 +880,8 @@ struct StereoOut {
     Poison err;                 // the block's error words (persistent PLL launch, release timeout)
 };
 
-#ifndef SDR_STO_WPE
-#define SDR_STO_WPE 1
-#endif
 template <int D>
-__global__ __launch_bounds__(AT) __attribute__((amdgpu_waves_per_eu(SDR_STO_WPE))) void k_stereo_out(const StereoOut a) {
+__global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
     constexpr int WIN = audio_win<D>(), TW = audio_tw<D>();
     __shared__ __attribute__((aligned(16))) float sa[(WIN + 3) / 4 * 4 + 4];
     __shared__ __attribute__((aligned(16))) float sb[(WIN + 3) / 4 * 4 + 4];
