@@ -30,7 +30,7 @@ constexpr int DEC_STATE = 8;     // ints of RDS decoder state per channel
 // MFMA front end (sdr_frontend.hip): digit planes of the fixed-point taps and tap fragments
 constexpr int FT_ND = 4;
 constexpr int FT_AFRAGS = 4 * FT_ND;
-constexpr int FT_NB = 32;        // 16-output blocks per wave tile
+constexpr int FT_NB = 32;        // 16-output blocks per wave tile (16, 48, 64: slower, profiles/r05/mfma_tile_ab.txt)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef int v4i __attribute__((ext_vector_type(4)));
