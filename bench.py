@@ -224,6 +224,7 @@ class GpuStepper:
         self.pll_start, self.pll_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
         self.gather_done = [ev() for _ in range(nblocks)]
         self.pre_done, self.post_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
+        self.post_dsp_done = [ev() for _ in range(nblocks)]   # block b's post DSP (before its captures)
         # the front end of block b also waits for block b-2's whole post stream work (the RDS chain
         # after its mixer, the output copies and captures included), not only for the library's own
         # parity release (its readers' first kernels): the front end then runs beside the PLL alone
@@ -234,6 +235,8 @@ class GpuStepper:
         # lengthens its critical path (2048 channels: 143.0 against 148.7 GS/s), so there the
         # release alone orders the front end.
         self.fe_waits_post = os.environ.get("SDR_BENCH_FE_WAIT", "post" if nch <= 1024 else "library") == "post"
+        # that wait covers block b-2's post DSP only, not its output captures (SDR_BENCH_FE_GATE=all: those too)
+        self.fe_gate_all = os.environ.get("SDR_BENCH_FE_GATE", "dsp") == "all"
         # outputs of a few channels, captured on the producing streams for the check after timing
         nv = min(VERIFY_CHANNELS, nch)
         self.vsel = torch.tensor(sorted({int(round(i * (nch - 1) / max(1, nv - 1))) for i in range(nv)}),
@@ -309,7 +312,7 @@ class GpuStepper:
         # for the release counts that block b-2's mono, stereo post and RDS mixer stored on theirs
         # (the RDS chain after its mixer and the output captures are not waited for)
         if b >= 2 and self.fe_waits_post:
-            s_fe.wait_event(self.post_done[b - 2])
+            s_fe.wait_event((self.post_done if self.fe_gate_all else self.post_dsp_done)[b - 2])
         # that wait (a one-wave kernel) goes ahead of the timer, so fe_start..fe_end spans the
         # front-end kernel alone (the roofline's average launch time; frontend() then waits no more)
         pipe.release_wait(stream=s_fe)
@@ -353,6 +356,9 @@ class GpuStepper:
             s_st.wait_event(self.ev_fork)
         pipe.stereo_post(lr, stream=s_st)                     # stereo.cpp:83-107
         pipe.rds_post(self.clean, bits=True, stream=s_post, bits_out=bits)   # rds.cpp:122-167
+        if s_st is s_post:
+            # the front end of block b + 2 waits for this, not for the output captures below
+            self.post_dsp_done[b].record(s_post)
         with torch.cuda.stream(s_post):
             torch.index_select(bits, 0, self.vsel, out=self.cap_bits[b])
             torch.index_select(pipe.nbits, 0, self.vsel, out=self.cap_nbits[b])
@@ -361,6 +367,7 @@ class GpuStepper:
         if s_st is not s_post:
             self.ev_join.record(s_st)
             s_post.wait_event(self.ev_join)
+            self.post_dsp_done[b].record(s_post)
         self.post_done[b].record(s_post)
         if gather is not None:
             # final audio / bitstream gather to rank 0 over RCCL (xGMI), on its own non-blocking
