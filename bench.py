@@ -501,7 +501,9 @@ class GpuStepper:
             rows["pll_gap"].append((ts[j] - te[j - 1]) * 1e-2)
         if not rows["fe"]:
             return None
-        return {k: round(float(np.median(v)), 1) for k, v in rows.items()}
+        out = {k: round(float(np.median(v)), 1) for k, v in rows.items()}
+        out["max"] = {k: round(float(np.max(v)), 1) for k, v in rows.items()}
+        return out
 
     @staticmethod
     def _pll_issue(cyc) -> dict:
