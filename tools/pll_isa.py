@@ -74,7 +74,8 @@ def main() -> None:
         if re.match(r"s_(cbranch|branch)", p[0]):
             blocks.append(cur)
             cur = []
-    chunk = next(b for b in blocks if sum(x[0] == "v_bitop3_b32" for x in b) == 16
+    # (16 more bitop3 with the base-angle table of SDR_PLL_BASETAB)
+    chunk = next(b for b in blocks if sum(x[0] == "v_bitop3_b32" for x in b) in (16, 32)
                  and sum(x[0] == "ds_read_b128" for x in b) >= 8)
     steps = 16
     cnt = {"VALU": 0, "SALU": 0, "LDS": 0, "s_nop": 0, "VMEM": 0}
