@@ -8,6 +8,11 @@ TAG=${TAG:-r02}
 O=gpurun_out/$TAG
 mkdir -p $O
 step() { echo "[$(date +%T)] $*"; }
+if [ "${SMOKE:-1}" = 1 ]; then
+  step smoke
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1; rc=$?
+  tail -2 $O/smoke.log; [ $rc -eq 0 ] || { tail -30 $O/smoke.log; exit $rc; }
+fi
 if [ "${TESTS:-1}" = 1 ]; then
   step tests
   timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
@@ -21,9 +26,12 @@ fi
 if [ "${PROF:-1}" = 1 ]; then
   step rocprof kernel-trace
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
-      python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-isolated ${BENCH_ARGS:-} > $O/prof.log 2>&1; rc=$?
+      python3 bench.py --steps 20 --warmup ${PROF_WARMUP:-5} --no-cpu-baseline --no-isolated > $O/prof.log 2>&1; rc=$?
   [ $rc -eq 0 ] || { tail -20 $O/prof.log; exit $rc; }
   find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+  find $O/prof -name "*kernel_trace.csv" -exec cp {} $O/kernel_trace.csv \;
+  grep '^{' $O/prof.log | tail -1 > $O/bench_profiled.json
+  python tools/timeline.py $O/kernel_trace.csv --by-grid k_frontend2 > $O/frontend_by_grid.txt && cat $O/frontend_by_grid.txt
   rm -rf $O/prof   # raw traces: gpurun_out/ is only copied back below 64 MiB
   head -14 $O/kernel_stats.csv | cut -c1-160
 fi

@@ -31,8 +31,10 @@ def load(path: pathlib.Path, counter: str) -> dict:
 
 
 def kernel_name(name: str) -> str:
-    # "void (anonymous namespace)::k_frontend2<8, 10, false>(...)" -> "k_frontend2<8, 10, false>"
-    return name.split("::", 1)[-1].split("(", 1)[0]
+    # "void sdrk::(anonymous namespace)::k_frontend2<8, 10>(...)" -> "k_frontend2<8, 10>"
+    for pre in ("void ", "sdrk::", "(anonymous namespace)::"):
+        name = name.replace(pre, "")
+    return name.split("(", 1)[0]
 
 
 def mode_of(name: str) -> str:
