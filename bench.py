@@ -168,11 +168,16 @@ class GpuStepper:
         s_fe, s_pll, s_post = (torch.cuda.Stream(dev, priority=-1 if n in prio else 0)
                                for n in ("fe", "pll", "post"))
         s_all = None
-        # SDR_BENCH_CUMASK=<n> (default 64; 0 = no masks): the PLL stream gets CUs [0, n), the
-        # front-end and post streams the complement, so that no other kernel shares a CU's issue
-        # slots with the PLL's lone waves (profiles/r01/ab_cumask.txt).
+        # SDR_BENCH_CUMASK=<n> (0 = no masks): the PLL stream gets CUs [0, n), the front-end and
+        # post streams the complement, so that no other kernel shares a CU's issue slots with the
+        # PLL's waves (profiles/r01/ab_cumask.txt). Default: 64 CUs up to 1024 channels (one wave
+        # per CU: the PLL's latency bounds the step), beyond that four waves per CU (the packed
+        # groups' LDS-staged loop, 262 cycles per step), so that the side chain, which then sets
+        # the period, keeps the most CUs: 2048 channels 148-150 GS/s on 64 CUs, 155.4 on 32
+        # (profiles/r05/coal/).
         self.created: list[int] = []
-        cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64")
+        pll_waves = 2 * ((2 * nch + 63) // 64)
+        cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64" if nch <= 1024 else str(min(64, max(16, pll_waves // 4))))
         if cu_spec not in ("", "0"):
             try:
                 # the all-CU fill/drain stream is a fourth dedicated hardware queue: at N > 1 RCCL's

@@ -740,6 +740,168 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// COAL: the lane-pair loop for waves that share a CU (capacity launches, more than one PLL wave per
+// CU). Per-lane row loads -- every lane reads 16 bytes of its own row, so each wave-instruction
+// touches 64 cache lines -- saturate the CU's texture addresser once several waves issue them
+// (209 -> 236 -> ~390 cycles per step at 1, 2, 4 waves per CU). Here a chunk's inputs
+// reach LDS by LDS-DMA (global_load_lds_dwordx4) in line-shaped pieces -- 16 x-rows x 64 B or 8
+// rx-rows x 128 B per instruction -- two chunks ahead, each lane then reads its own rows from LDS,
+// and the 16 phases go out the same way in reverse (own row into LDS, line-shaped pieces out). The
+// one-wave-per-CU path (the headline) keeps the register prefetch, which needs no LDS round trip.
+// Layout of one buffer: 8 pieces of 1 KiB at a 1040-byte pitch (a 16-byte rotation per piece keeps
+// the own-row reads free of bank conflicts): pieces 0-3 hold x-rows r with r % 4 = k, pieces 4-7
+// the rx rows q with q % 4 = k. Every lane of the wave must run the loop (all 32 channels valid).
+// ------------------------------------------------------------------------------------------
+#ifndef SDR_PLL_COAL
+#define SDR_PLL_COAL 1
+#endif
+constexpr int COAL_PIECE = 1040;
+constexpr int COAL_BUF = 8 * COAL_PIECE;
+constexpr int COAL_TROW = 80;                         // t staging: 32 rows of 64 B at an 80-byte pitch
+
+template <bool TAB, bool GATE>
+__device__ __forceinline__ void pll_run_split_coal(const PllJob& jb, int n, int ch, const double* __restrict__ wtab,
+                                                   InGate* gate, uint8_t* __restrict__ lbuf,
+                                                   uint8_t* __restrict__ ltst) {
+    const SplitLane L = split_lane();
+    const int lane = threadIdx.x & 63;
+    const int chw0 = ch - (lane >> 1);                 // the wave's first channel
+    const size_t t_stride = jb.t_stride, out_stride = jb.out_stride;
+    sdr_pll_state* __restrict__ st = jb.st;
+    const float freq = jb.freq, Fs = jb.Fs, normBandwidth = jb.bw;
+    const float Cp = 2.666;
+    const float Ci = 3.555;
+    const float Kp = normBandwidth * Cp;
+    const float Ki = normBandwidth * normBandwidth * Ci;
+    const double w = 2 * 3.14159265358979323846 * (freq / Fs);
+    const sdr_pll_state s0 = st[ch];
+    const float* xpos = jb.in + (size_t)ch * jb.in_stride;
+    const double* rxp = jb.rx + (size_t)ch * jb.rx_stride;
+    float* tb = jb.tbuf + (size_t)ch * t_stride;
+    if (!jb.prev_out && L.a) jb.out[(size_t)ch * out_stride] = s0.lastCarrier;   // pll.cpp:18
+    SplitRegs r = full_to_split(pll_load(s0, w), L.a);
+    constexpr int C = PLL_CHUNK;
+    static_assert(C == 16, "COAL pieces: 16 samples per row and chunk");
+    const int nchunks = n / C;
+    const int nmain = nchunks - nchunks % 2;
+    // this lane's pieces: x-row 4 (lane / 4) + k (even rows: -x of channel row / 2, odd: x), floats
+    // 4 (lane % 4) ..; rx row 4 (lane / 8) + k, doubles 2 (lane % 8) ..
+    const float* xsrc[4];
+    const double* rsrc[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int xr = 4 * (lane >> 2) + k, c = chw0 + (xr >> 1);
+        xsrc[k] = ((xr & 1) ? jb.in + (size_t)c * jb.in_stride : jb.in_neg + (size_t)c * jb.neg_stride) + 4 * (lane & 3);
+        rsrc[k] = jb.rx + (size_t)(chw0 + 4 * (lane >> 3) + k) * jb.rx_stride + 2 * (lane & 7);
+    }
+    auto issue = [&](int b, int i0) {                  // chunk at sample i0 -> buffer b (LDS-DMA)
+        uint8_t* base = lbuf + b * COAL_BUF;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(xsrc[k] + i0), base + k * COAL_PIECE, 16, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(rsrc[k] + i0), base + (4 + k) * COAL_PIECE,
+                                             16, 0, 0);
+    };
+    float xb[C];
+    double rb[C];
+    auto take = [&](int b) {                            // this lane's rows of buffer b
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint8_t* base = lbuf + b * COAL_BUF;
+        const uint8_t* xr = base + (lane & 3) * COAL_PIECE + (lane >> 2) * 64;
+        const int q = lane >> 1;
+        const uint8_t* rr = base + (4 + (q & 3)) * COAL_PIECE + (q >> 2) * 128;
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + 16 * p);
+            xb[4 * p] = v.x; xb[4 * p + 1] = v.y; xb[4 * p + 2] = v.z; xb[4 * p + 3] = v.w;
+        }
+#pragma unroll
+        for (int p = 0; p < 8; p++) {
+            const double2 v = *reinterpret_cast<const double2*>(rr + 16 * p);
+            rb[2 * p] = v.x; rb[2 * p + 1] = v.y;
+        }
+    };
+    if (nmain > 0) {
+        if (GATE) gate_wait(*gate, 2 * C);
+        issue(0, 0);
+        issue(1, C);
+        take(0);
+    }
+    for (int c0 = 0; c0 < nmain; c0 += 2) {
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int c = c0 + u, i0 = c * C;
+            double wv[C];
+            if (TAB) {
+#pragma unroll
+                for (int k = 0; k < C / 2; k++) {
+                    const double2 v = reinterpret_cast<const double2*>(wtab + i0)[k];
+                    wv[2 * k] = v.x; wv[2 * k + 1] = v.y;
+                }
+            }
+            const SplitRegs snap = r;
+            PllProof pf;
+            float tv[C];
+#pragma unroll
+            for (int j = 0; j < C; j++)
+                pll_step_split<TAB>(r, xb[j], rb[j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf, L);
+            const bool ok = (pf.emaxf < PLL_EMAX_F) & (pf.split == 0u) & (pf.tie > pllm::TIE_MIN) &
+                            (__builtin_fabs(r.ip.y) < 0x1p28f) & (__builtin_fabs(r.ip.x) < 0x1p20f) &
+                            (TAB || (pf.tmax < 0x1p30f));
+            const int ok_partner = __builtin_amdgcn_mov_dpp((int)ok, 0xB1, 0xF, 0xF, false);
+            const bool pair_ok = ok & (ok_partner != 0);
+            if (!pair_ok) {
+                PllRegs full = split_to_full(snap, L.a);
+#pragma unroll
+                for (int j = 0; j < C; j++)
+                    pll_step<true, TAB>(full, L.a ? -xb[j] : xb[j], rb[j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf);
+                r = full_to_split(full, L.a);
+            }
+            // the next chunk's rows (its DMA went out a chunk ago), then this chunk's phases out: the
+            // even lanes' rows (both lanes of a pair hold the same phases) into LDS, line-shaped
+            // pieces back: lane l stores 16 B of channel row 16 k + l / 4
+            if (c + 1 < nmain) take(u ^ 1);
+            if (L.a) {
+#pragma unroll
+                for (int p = 0; p < 4; p++)
+                    *reinterpret_cast<float4*>(ltst + (lane >> 1) * COAL_TROW + 16 * p) =
+                        make_float4(tv[4 * p], tv[4 * p + 1], tv[4 * p + 2], tv[4 * p + 3]);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int q = 16 * k + (lane >> 2);
+                const float4 v = *reinterpret_cast<const float4*>(ltst + q * COAL_TROW + 16 * (lane & 3));
+                *reinterpret_cast<float4*>(jb.tbuf + (size_t)(chw0 + q) * t_stride + i0 + 4 * (lane & 3)) = v;
+            }
+            if (c + 2 < nmain) {
+                if (GATE) gate_wait(*gate, (c + 3) * C);
+                issue(u, (c + 2) * C);
+            }
+        }
+    }
+    PllRegs full = split_to_full(r, L.a);
+    {
+        // the rest (< 2 chunks + n % C steps): full checked steps on both lanes of the pair
+        PllProof pf;
+        const int i_rest = nmain * C;
+        if (GATE) gate_wait(*gate, n);
+        for (int i = i_rest; i < n; i++)
+            pll_step<true, TAB>(full, xpos[i], rxp[i], Kp, Ki, w, TAB ? wtab[i] : 0.0, tb[i], pf);
+    }
+    if (TAB) full.toff = s0.trigOffset + (double)n;            // pll.cpp:46, n times (exact)
+    if (L.a) {   // every field but lastCarrier (the NCO's); the feedback back in the frame of t
+        pllm::rot_q(1u - full.nq1, full.fbI, full.fbQ);
+        st[ch].feedbackI = full.fbI;
+        st[ch].feedbackQ = full.fbQ;
+        st[ch].integrator = full.ip.x;
+        st[ch].phaseEst = full.ip.y;
+        st[ch].trigOffset = full.toff;
+    }
+}
+
 // VEC: x / rx rows and the t buffer are 16-byte aligned with strides that are multiples of 4
 // (x, t) and 2 (rx), so a chunk's inputs are prefetched with 16-byte loads and the 16 phases are
 // stored with 16-byte stores -- the unrolled chunk itself touches no memory.
@@ -812,16 +974,22 @@ __global__ __launch_bounds__(64) void k_pll(const PllJobs jobs, int n, int nch, 
 // LDS (all channels of a context advance together, so one table serves every wave whose lanes share
 // the group's trigOffset), its wave 0 polls the block flag, and two barriers per block keep the
 // group's waves on the same block (the table is rebuilt only after every wave finished reading it).
-template <bool VEC, bool SPLIT, int WG>
+template <bool VEC, bool SPLIT, int WG, bool COAL = false>
 __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int n, int nch, int tab_ok, int nblocks,
                                                        const uint32_t* pre_flag, uint32_t pre_first,
                                                        uint32_t* done_ring, uint32_t* err,
                                                        unsigned long long* t_start, unsigned long long* t_end,
                                                        unsigned long long* t_cyc, const uint32_t* sub_flag,
                                                        uint32_t sub_base, int sub_tile) {
+    static_assert(!COAL || (VEC && SPLIT), "COAL: the lane-pair loop with 16-byte rows");
     extern __shared__ double wtab[];
     __shared__ double sh_toff;
     __shared__ int sh_dead;
+    // COAL: per wave two DMA buffers and the phase staging rows (pll_run_split_coal)
+    __shared__ __attribute__((aligned(16))) uint8_t coal_buf[COAL ? WG * 2 * COAL_BUF : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t coal_tst[COAL ? WG * 32 * COAL_TROW : 16];
+    uint8_t* const my_buf = coal_buf + (COAL ? (threadIdx.x >> 6) * 2 * COAL_BUF : 0);
+    uint8_t* const my_tst = coal_tst + (COAL ? (threadIdx.x >> 6) * 32 * COAL_TROW : 0);
     const int lg = blockIdx.x * blockDim.x + threadIdx.x;
     const int ch = SPLIT ? lg >> 1 : lg;
     const bool active = ch < nch;
@@ -905,6 +1073,9 @@ __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int 
                         gate_wait(g, 1);      // the part(s) the wait above saw
                         if (tab) pll_run_split<VEC, true, true>(jb, n, ch, wtab, &g);
                         else pll_run_split<VEC, false, true>(jb, n, ch, nullptr, &g);
+                    } else if constexpr (COAL) {
+                        if (tab) pll_run_split_coal<true, false>(jb, n, ch, wtab, nullptr, my_buf, my_tst);
+                        else pll_run_split_coal<false, false>(jb, n, ch, nullptr, nullptr, my_buf, my_tst);
                     } else {
                         if (tab) pll_run_split<VEC, true>(jb, n, ch, wtab);
                         else pll_run_split<VEC, false>(jb, n, ch, nullptr);
@@ -1136,6 +1307,11 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
     const int WG = (max_cus > 0 && wave_cnt > 2 * max_cus) ? 4 : 1;
     const dim3 g(cdiv(split ? 2 * nch : nch, 64 * WG), 2), b(64 * WG);
     *waves = g.x * g.y * WG;
+    // packed groups (more than two waves per CU): the chunk inputs and phases through LDS in
+    // line-shaped pieces (pll_run_split_coal; every lane of every wave must hold a channel): 357 -> 262
+    // cycles per step at four waves per CU; at two it measured 231-235 -> 237, so one-wave groups keep
+    // the register prefetch (profiles/r05/coal/)
+    const bool coal = SDR_PLL_COAL && vec && split && nch % 32 == 0 && WG == 4;
     auto kern_of = [&](auto v, auto sp, auto wg) -> const void* {
         return reinterpret_cast<const void*>(k_pll_multi<decltype(v)::value, decltype(sp)::value, decltype(wg)::value>);
     };
@@ -1143,7 +1319,9 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
     using F = std::false_type;
     using W1 = std::integral_constant<int, 1>;
     using W4 = std::integral_constant<int, 4>;
-    const void* kern = WG == 4 ? (vec ? (split ? kern_of(T{}, T{}, W4{}) : kern_of(T{}, F{}, W4{}))
+    const void* kern = coal ? (WG == 4 ? reinterpret_cast<const void*>(k_pll_multi<true, true, 4, true>)
+                                       : reinterpret_cast<const void*>(k_pll_multi<true, true, 1, true>))
+                     : WG == 4 ? (vec ? (split ? kern_of(T{}, T{}, W4{}) : kern_of(T{}, F{}, W4{}))
                                       : (split ? kern_of(F{}, T{}, W4{}) : kern_of(F{}, F{}, W4{})))
                                : (vec ? (split ? kern_of(T{}, T{}, W1{}) : kern_of(T{}, F{}, W1{}))
                                       : (split ? kern_of(F{}, T{}, W1{}) : kern_of(F{}, F{}, W1{})));

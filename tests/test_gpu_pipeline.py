@@ -657,16 +657,19 @@ def test_persistent_plls_signal_checks_block_order(pkg, synth, torch_cuda, own_q
     pipe.close()
 
 
-def test_persistent_plls_packed_groups_match_sequential(pkg, synth, torch_cuda):
-    """More PLL waves than two per CU of the PLL stream: the persistent launch packs them in groups of
-    four (one wave per SIMD) sharing one trigArg table per CU (512 channels = 32 waves on an 8-CU
-    stream); audio, rds_clean and RDS bits equal the one-stream pipeline's, block by block."""
+@pytest.mark.parametrize("nch", [512, 256])
+def test_persistent_plls_packed_groups_match_sequential(pkg, synth, torch_cuda, nch):
+    """More PLL waves than CUs of the PLL stream: 512 channels = 32 waves on an 8-CU stream, packed in
+    groups of four (one wave per SIMD) sharing one trigArg table per CU, whose blocks after the fill
+    run the chunk loop that stages inputs and phases through LDS (pll_run_split_coal); 256 channels
+    = 16 waves, two one-wave groups per CU (the register-prefetch loop). Audio, rds_clean and RDS
+    bits equal the one-stream pipeline's, block by block."""
     import ctypes as C
     import sys
     sys.path.insert(0, str(ROOT))
     import bench
     torch = torch_cuda
-    nch, nb = 512, 4
+    nb = 4
     d = bench.make_input(torch, nch, nb, first_channel=700, device=torch.device("cuda", 0))   # distinct channels
     ref = {"stereo": [], "clean": [], "bits": [], "nbits": []}
     one = pkg.Pipeline(nch)                         # the one-stream pipeline on the same bytes
