@@ -81,6 +81,28 @@ def launch_ranks(args, argv: list[str]) -> int:
 
 
 # ------------------------------------------------------------------------------ GPU stepper
+def pll_cus(nch: int) -> int:
+    """CUs for the PLL stream: 1, 2 or 4 PLL waves per CU, whichever bounds the block period least
+    by a two-term model fitted to this round's lines (profiles/r05/coal/, capacity/): the PLL's step at
+    k waves per CU (209, 233, 263 shader cycles; 7350 steps at ~2.3 GHz) against the side chain's
+    ~0.106 ms x channels / (CUs left). 1024 channels -> 64 CUs (one wave per CU, the headline),
+    2048 -> 32 and 4096 -> 64 (four: the packed groups' LDS-staged loop)."""
+    waves = 2 * ((2 * nch + 63) // 64)
+    best = None
+    # masks of 16, 32, 64 or 128 CUs only: a persistent launch needs every wave resident at once, and a
+    # 48-CU mask left waves of a 1536-channel launch (2 per CU) unplaced until the bounded waits
+    # expired (SDR_E_TIMEOUT, profiles/r05/coal/), although its CU count passed the library's check
+    for cus in (16, 32, 64, 128):
+        k = (waves + cus - 1) // cus
+        if k > 4:
+            continue
+        cyc = 209.0 if k <= 1 else 233.0 if k <= 2 else 263.0
+        period = max(7350 * cyc / 2.3e6, 0.106 * nch / (256 - cus))
+        if best is None or period < best[0] - 1e-9:
+            best = (period, cus)
+    return best[1] if best else 64
+
+
 def cu_masked_streams(torch, pkg, dev, spec: str, created: list, all_cus: bool = True):
     """(fe, pll, post, all) streams through the C ABI (sdr_stream_create_cu_range): the PLL stream
     on CUs [0, n), front end and post on the rest, and one stream over every CU for the pipeline's
@@ -170,14 +192,9 @@ class GpuStepper:
         s_all = None
         # SDR_BENCH_CUMASK=<n> (0 = no masks): the PLL stream gets CUs [0, n), the front-end and
         # post streams the complement, so that no other kernel shares a CU's issue slots with the
-        # PLL's waves (profiles/r01/ab_cumask.txt). Default: 64 CUs up to 1024 channels (one wave
-        # per CU: the PLL's latency bounds the step), beyond that four waves per CU (the packed
-        # groups' LDS-staged loop, 262 cycles per step), so that the side chain, which then sets
-        # the period, keeps the most CUs: 2048 channels 148-150 GS/s on 64 CUs, 155.4 on 32
-        # (profiles/r05/coal/).
+        # PLL's waves (profiles/r01/ab_cumask.txt). Default: pll_cus(nch).
         self.created: list[int] = []
-        pll_waves = 2 * ((2 * nch + 63) // 64)
-        cu_spec = os.environ.get("SDR_BENCH_CUMASK", "64" if nch <= 1024 else str(min(64, max(16, pll_waves // 4))))
+        cu_spec = os.environ.get("SDR_BENCH_CUMASK", str(pll_cus(nch)))
         if cu_spec not in ("", "0"):
             try:
                 # the all-CU fill/drain stream is a fourth dedicated hardware queue: at N > 1 RCCL's
