@@ -1,0 +1,19 @@
+# Round 5 session Z: the packed groups' LDS-staged PLL loop with plain 16-byte loads + ds_write
+# (register staging, coalrs) against LDS-DMA (default): parity of the packed-group test under
+# coalrs, then 20-step lines at 4 waves per CU (1024@16, 2048@32) and forced at 1 wave per CU
+# (coalall / coalrsall, 1024@64), 2 interleaved rounds.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r05_z}
+mkdir -p $O
+SDR_AMD_LIB=$PWD/build/variants/coalrs.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+  tests/test_gpu_pipeline.py -k "packed_groups or persistent" > $O/pytest_coalrs.txt 2>&1 || { echo "parity FAILED"; tail -30 $O/pytest_coalrs.txt; exit 1; }
+echo "coalrs parity: $(tail -1 $O/pytest_coalrs.txt)"
+for r in 1 2; do
+  for cfg in "1024 16 default" "1024 16 coalrs" "2048 32 default" "2048 32 coalrs" "1024 64 coalall" "1024 64 coalrsall"; do
+    set -- $cfg
+    if [ $3 = default ]; then unset SDR_AMD_LIB; else export SDR_AMD_LIB=$PWD/build/variants/$3.so; fi
+    SDR_BENCH_CUMASK=$2 timeout -k 10 300 python bench.py --channels $1 --steps 20 --warmup 5 --no-cpu-baseline --no-isolated > $O/b_$1_$2_$3_$r.json 2> $O/b_$1_$2_$3_$r.err || { tail -5 $O/b_$1_$2_$3_$r.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/b_$1_$2_$3_$r.json')); p=d['pll']; print('$1@$2 $3', d['value'], d['ms_per_step'], p.get('cycles_per_step'), p.get('shader_clock_mhz'), p.get('timeline',{}).get('pll_idle_ms'))"
+  done
+done
