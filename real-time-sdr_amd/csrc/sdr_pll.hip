@@ -753,9 +753,6 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
 // the own-row reads free of bank conflicts): pieces 0-3 hold x-rows r with r % 4 = k, pieces 4-7
 // the rx rows q with q % 4 = k. Every lane of the wave must run the loop (all 32 channels valid).
 // ------------------------------------------------------------------------------------------
-#ifndef SDR_PLL_COAL
-#define SDR_PLL_COAL 1   // 0: never, 2: one-wave groups too (A/B)
-#endif
 constexpr int COAL_PIECE = 1040;
 constexpr int COAL_BUF = 8 * COAL_PIECE;
 constexpr int COAL_TROW = 80;                         // t staging: 32 rows of 64 B at an 80-byte pitch
@@ -1311,7 +1308,7 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
     // line-shaped pieces (pll_run_split_coal; every lane of every wave must hold a channel): 357 -> 262
     // cycles per step at four waves per CU; at two it measured 231-235 -> 237, so one-wave groups keep
     // the register prefetch (profiles/r05/coal/)
-    const bool coal = SDR_PLL_COAL && vec && split && nch % 32 == 0 && (WG == 4 || SDR_PLL_COAL == 2);
+    const bool coal = vec && split && nch % 32 == 0 && WG == 4;
     auto kern_of = [&](auto v, auto sp, auto wg) -> const void* {
         return reinterpret_cast<const void*>(k_pll_multi<decltype(v)::value, decltype(sp)::value, decltype(wg)::value>);
     };

@@ -1,6 +1,6 @@
 # Round 5 session W: the PLL chunk loop through LDS for waves that share a CU (pll_run_split_coal):
 # parity (pipeline tests incl. the packed-group launches at 2 and 4 waves per CU), then capacity
-# lines with and without it (SDR_PLL_COAL=0 variant), 20 steps, 2 interleaved rounds.
+# lines with and without it (SDR_PLL_COAL=0 variant: tools/patches/pll_coal_knob.patch restores the knob), 20 steps, 2 interleaved rounds.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r05_w}
