@@ -749,9 +749,10 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
 // rx-rows x 128 B per instruction -- two chunks ahead, each lane then reads its own rows from LDS,
 // and the 16 phases go out the same way in reverse (own row into LDS, line-shaped pieces out). The
 // one-wave-per-CU path (the headline) keeps the register prefetch, which needs no LDS round trip.
-// Layout of one buffer: 8 pieces of 1 KiB at a 1040-byte pitch (a 16-byte rotation per piece keeps
-// the own-row reads free of bank conflicts): pieces 0-3 hold x-rows r with r % 4 = k, pieces 4-7
-// the rx rows q with q % 4 = k. Every lane of the wave must run the loop (all 32 channels valid).
+// Layout of one buffer: pieces of 1 KiB at a 1040-byte pitch (a 16-byte rotation per piece keeps
+// the own-row reads free of bank conflicts): pieces 0-1 hold the x rows of channels q with q % 2 = k
+// (lane A, which runs on -x, flips the sign bit as it reads), pieces 4-7 the rx rows q with
+// q % 4 = k. Every lane of the wave must run the loop (all 32 channels valid).
 // ------------------------------------------------------------------------------------------
 constexpr int COAL_PIECE = 1040;
 constexpr int COAL_BUF = 8 * COAL_PIECE;
@@ -784,18 +785,22 @@ __device__ __forceinline__ void pll_run_split_coal(const PllJob& jb, int n, int 
     const int nmain = nchunks - nchunks % 2;
     // this lane's pieces: x-row 4 (lane / 4) + k (even rows: -x of channel row / 2, odd: x), floats
     // 4 (lane % 4) ..; rx row 4 (lane / 8) + k, doubles 2 (lane % 8) ..
-    const float* xsrc[4];
+    // the x rows only (channel row 2 (lane / 4) + k in piece k; lane A flips the sign on the read):
+    // 6 pieces per chunk instead of 8 with the -x rows, 262-267 -> 260-263 cycles per step
+    // (profiles/r05/coal/xonly/)
+    constexpr int NXP = 2;
+    const float* xsrc[NXP];
+#pragma unroll
+    for (int k = 0; k < NXP; k++)
+        xsrc[k] = jb.in + (size_t)(chw0 + 2 * (lane >> 2) + k) * jb.in_stride + 4 * (lane & 3);
     const double* rsrc[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int xr = 4 * (lane >> 2) + k, c = chw0 + (xr >> 1);
-        xsrc[k] = ((xr & 1) ? jb.in + (size_t)c * jb.in_stride : jb.in_neg + (size_t)c * jb.neg_stride) + 4 * (lane & 3);
+    for (int k = 0; k < 4; k++)
         rsrc[k] = jb.rx + (size_t)(chw0 + 4 * (lane >> 3) + k) * jb.rx_stride + 2 * (lane & 7);
-    }
     auto issue = [&](int b, int i0) {                  // chunk at sample i0 -> buffer b (LDS-DMA)
         uint8_t* base = lbuf + b * COAL_BUF;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < NXP; k++)
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(xsrc[k] + i0), base + k * COAL_PIECE, 16, 0, 0);
 #pragma unroll
         for (int k = 0; k < 4; k++)
@@ -807,13 +812,17 @@ __device__ __forceinline__ void pll_run_split_coal(const PllJob& jb, int n, int 
     auto take = [&](int b) {                            // this lane's rows of buffer b
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint8_t* base = lbuf + b * COAL_BUF;
-        const uint8_t* xr = base + (lane & 3) * COAL_PIECE + (lane >> 2) * 64;
         const int q = lane >> 1;
+        const uint8_t* xr = base + (q & 1) * COAL_PIECE + (q >> 1) * 64;
+        const uint32_t flip = L.a ? 0x80000000u : 0u;      // lane A: -x (exact)
         const uint8_t* rr = base + (4 + (q & 3)) * COAL_PIECE + (q >> 2) * 128;
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            const float4 v = *reinterpret_cast<const float4*>(xr + 16 * p);
-            xb[4 * p] = v.x; xb[4 * p + 1] = v.y; xb[4 * p + 2] = v.z; xb[4 * p + 3] = v.w;
+            const uint4 v = *reinterpret_cast<const uint4*>(xr + 16 * p);
+            xb[4 * p] = __builtin_bit_cast(float, v.x ^ flip);
+            xb[4 * p + 1] = __builtin_bit_cast(float, v.y ^ flip);
+            xb[4 * p + 2] = __builtin_bit_cast(float, v.z ^ flip);
+            xb[4 * p + 3] = __builtin_bit_cast(float, v.w ^ flip);
         }
 #pragma unroll
         for (int p = 0; p < 8; p++) {
