@@ -746,8 +746,9 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
 // touches 64 cache lines -- saturate the CU's texture addresser once several waves issue them
 // (209 -> 236 -> ~390 cycles per step at 1, 2, 4 waves per CU). Here a chunk's inputs
 // reach LDS by LDS-DMA (global_load_lds_dwordx4) in line-shaped pieces -- 16 x-rows x 64 B or 8
-// rx-rows x 128 B per instruction -- two chunks ahead, each lane then reads its own rows from LDS,
-// and the 16 phases go out the same way in reverse (own row into LDS, line-shaped pieces out). The
+// rx-rows x 128 B per instruction -- two chunks ahead into a ring of three LDS buffers, each lane then
+// reads its own rows from LDS, and the 16 phases go out the same way in reverse (own row into LDS,
+// line-shaped pieces out). The
 // one-wave-per-CU path (the headline) keeps the register prefetch, which needs no LDS round trip.
 // Layout of one buffer: pieces of 1 KiB at a 1040-byte pitch (a 16-byte rotation per piece keeps
 // the own-row reads free of bank conflicts): pieces 0-1 hold the x rows of channels q with q % 2 = k
@@ -755,7 +756,10 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
 // q % 4 = k. Every lane of the wave must run the loop (all 32 channels valid).
 // ------------------------------------------------------------------------------------------
 constexpr int COAL_PIECE = 1040;
-constexpr int COAL_BUF = 8 * COAL_PIECE;
+constexpr int COAL_BUF = 6 * COAL_PIECE;              // pieces 0-1: x rows, 2-5: rx rows
+// LDS buffers per wave: the DMA runs two chunks ahead (a ring of 2, one chunk ahead: 261-264 against
+// 258-261 cycles per step, profiles/r05/coal/ring/)
+constexpr int COAL_RING = 3;
 constexpr int COAL_TROW = 80;                         // t staging: 32 rows of 64 B at an 80-byte pitch
 
 template <bool TAB, bool GATE>
@@ -804,18 +808,21 @@ __device__ __forceinline__ void pll_run_split_coal(const PllJob& jb, int n, int 
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(xsrc[k] + i0), base + k * COAL_PIECE, 16, 0, 0);
 #pragma unroll
         for (int k = 0; k < 4; k++)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(rsrc[k] + i0), base + (4 + k) * COAL_PIECE,
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(rsrc[k] + i0), base + (2 + k) * COAL_PIECE,
                                              16, 0, 0);
     };
     float xb[C];
     double rb[C];
-    auto take = [&](int b) {                            // this lane's rows of buffer b
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this lane's rows of buffer b once its DMA has landed: with a ring of 3 the next chunk's 6 pieces
+    // (issued after it) may still be in flight; every chunk issues exactly 6 (the last ones re-read
+    // chunk nmain - 1 into spent buffers), so the count is exact
+    auto take = [&](int b) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         const uint8_t* base = lbuf + b * COAL_BUF;
         const int q = lane >> 1;
         const uint8_t* xr = base + (q & 1) * COAL_PIECE + (q >> 1) * 64;
         const uint32_t flip = L.a ? 0x80000000u : 0u;      // lane A: -x (exact)
-        const uint8_t* rr = base + (4 + (q & 3)) * COAL_PIECE + (q >> 2) * 128;
+        const uint8_t* rr = base + (2 + (q & 3)) * COAL_PIECE + (q >> 2) * 128;
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const uint4 v = *reinterpret_cast<const uint4*>(xr + 16 * p);
@@ -830,16 +837,19 @@ __device__ __forceinline__ void pll_run_split_coal(const PllJob& jb, int n, int 
             rb[2 * p] = v.x; rb[2 * p + 1] = v.y;
         }
     };
+    static_assert(!GATE, "COAL: not on the fill block (its input arrives in parts)");
     if (nmain > 0) {
-        if (GATE) gate_wait(*gate, 2 * C);
         issue(0, 0);
-        issue(1, C);
+        issue(1, min(1, nmain - 1) * C);
+        issue(2, min(2, nmain - 1) * C);
         take(0);
     }
+    int bc = 0;                                         // buffer of chunk c (c mod COAL_RING)
     for (int c0 = 0; c0 < nmain; c0 += 2) {
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const int c = c0 + u, i0 = c * C;
+            const int bn = bc + 1 == COAL_RING ? 0 : bc + 1;   // buffer of chunk c + 1
             double wv[C];
             if (TAB) {
 #pragma unroll
@@ -869,7 +879,7 @@ __device__ __forceinline__ void pll_run_split_coal(const PllJob& jb, int n, int 
             // the next chunk's rows (its DMA went out a chunk ago), then this chunk's phases out: the
             // even lanes' rows (both lanes of a pair hold the same phases) into LDS, line-shaped
             // pieces back: lane l stores 16 B of channel row 16 k + l / 4
-            if (c + 1 < nmain) take(u ^ 1);
+            if (c + 1 < nmain) take(bn);
             if (L.a) {
 #pragma unroll
                 for (int p = 0; p < 4; p++)
@@ -882,12 +892,11 @@ __device__ __forceinline__ void pll_run_split_coal(const PllJob& jb, int n, int 
                 const float4 v = *reinterpret_cast<const float4*>(ltst + q * COAL_TROW + 16 * (lane & 3));
                 *reinterpret_cast<float4*>(jb.tbuf + (size_t)(chw0 + q) * t_stride + i0 + 4 * (lane & 3)) = v;
             }
-            if (c + 2 < nmain) {
-                if (GATE) gate_wait(*gate, (c + 3) * C);
-                issue(u, (c + 2) * C);
-            }
+            issue(bc, min(c + 3, nmain - 1) * C);          // into chunk c's spent buffer
+            bc = bn;
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // spare pieces land before the buffers are reused
     PllRegs full = split_to_full(r, L.a);
     {
         // the rest (< 2 chunks + n % C steps): full checked steps on both lanes of the pair
@@ -992,9 +1001,9 @@ __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int 
     __shared__ double sh_toff;
     __shared__ int sh_dead;
     // COAL: per wave two DMA buffers and the phase staging rows (pll_run_split_coal)
-    __shared__ __attribute__((aligned(16))) uint8_t coal_buf[COAL ? WG * 2 * COAL_BUF : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t coal_buf[COAL ? WG * COAL_RING * COAL_BUF : 16];
     __shared__ __attribute__((aligned(16))) uint8_t coal_tst[COAL ? WG * 32 * COAL_TROW : 16];
-    uint8_t* const my_buf = coal_buf + (COAL ? (threadIdx.x >> 6) * 2 * COAL_BUF : 0);
+    uint8_t* const my_buf = coal_buf + (COAL ? (threadIdx.x >> 6) * COAL_RING * COAL_BUF : 0);
     uint8_t* const my_tst = coal_tst + (COAL ? (threadIdx.x >> 6) * 32 * COAL_TROW : 0);
     const int lg = blockIdx.x * blockDim.x + threadIdx.x;
     const int ch = SPLIT ? lg >> 1 : lg;
