@@ -1334,8 +1334,7 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
     using F = std::false_type;
     using W1 = std::integral_constant<int, 1>;
     using W4 = std::integral_constant<int, 4>;
-    const void* kern = coal ? (WG == 4 ? reinterpret_cast<const void*>(k_pll_multi<true, true, 4, true>)
-                                       : reinterpret_cast<const void*>(k_pll_multi<true, true, 1, true>))
+    const void* kern = coal ? reinterpret_cast<const void*>(k_pll_multi<true, true, 4, true>)
                      : WG == 4 ? (vec ? (split ? kern_of(T{}, T{}, W4{}) : kern_of(T{}, F{}, W4{}))
                                       : (split ? kern_of(F{}, T{}, W4{}) : kern_of(F{}, F{}, W4{})))
                                : (vec ? (split ? kern_of(T{}, T{}, W1{}) : kern_of(T{}, F{}, W1{}))

@@ -62,7 +62,7 @@ def main() -> None:
         dis = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", str(obj)], capture_output=True, text=True,
                              check=True).stdout
     lines = dis.split("\n")
-    start = next(i for i, l in enumerate(lines) if re.search(r"<.*k_pll_multiILb1ELb1ELi1E.*>:", l))
+    start = next(i for i, l in enumerate(lines) if re.search(r"<.*k_pll_multiILb1ELb1ELi1ELb0E.*>:", l))
     end = next(i for i in range(start + 1, len(lines)) if re.match(r"^[0-9a-f]+ <.*>:$", lines[i].strip()))
     # basic blocks of the kernel; the TAB fast chunk: 16 bitop3 and 8 ds_read_b128 (the table)
     blocks, cur = [], []
