@@ -81,25 +81,27 @@ def launch_ranks(args, argv: list[str]) -> int:
 
 
 # ------------------------------------------------------------------------------ GPU stepper
-def pll_cus(nch: int) -> int:
+def pll_cus(nch: int, fits, ncu: int = 256) -> int:
     """CUs for the PLL stream: 1, 2 or 4 PLL waves per CU, whichever bounds the block period least
-    by a two-term model fitted to this round's lines (profiles/r05/coal/, capacity/): the PLL's step at
+    by a two-term model fitted to round 5's lines (profiles/r05/coal/, capacity/): the PLL's step at
     k waves per CU (209, 233, 263 shader cycles; 7350 steps at ~2.3 GHz) against the side chain's
-    ~0.106 ms x channels / (CUs left). 1024 channels -> 64 CUs (one wave per CU, the headline),
-    2048 -> 32 and 4096 -> 64 (four: the packed groups' LDS-staged loop)."""
+    ~0.106 ms x channels / (CUs left); at equal periods fewer waves per CU, then fewer CUs. 1024
+    channels -> 64 CUs (one wave per CU, the headline), 2048 -> 32 and 4096 -> 64 (four: the packed
+    groups' LDS-staged loop). Only CU counts the library says a persistent launch can hold are
+    candidates: fits(n) asks sdr_plls_fits whether every workgroup is resident on CUs [0, n) at once
+    (a 48-CU mask falls unevenly on the shader engines and once left a 1536-channel launch waiting
+    until its bounded waits expired, profiles/r05/coal/forced/)."""
     waves = 2 * ((2 * nch + 63) // 64)
     best = None
-    # masks of 16, 32, 64 or 128 CUs only: a persistent launch needs every wave resident at once, and a
-    # 48-CU mask left waves of a 1536-channel launch (2 per CU) unplaced until the bounded waits
-    # expired (SDR_E_TIMEOUT, profiles/r05/coal/), although its CU count passed the library's check
-    for cus in (16, 32, 64, 128):
+    for cus in range(8, 129, 8):
         k = (waves + cus - 1) // cus
-        if k > 4:
+        if k > 4 or not fits(cus):
             continue
         cyc = 209.0 if k <= 1 else 233.0 if k <= 2 else 263.0
-        period = max(7350 * cyc / 2.3e6, 0.106 * nch / (256 - cus))
-        if best is None or period < best[0] - 1e-9:
-            best = (period, cus)
+        period = max(7350 * cyc / 2.3e6, 0.106 * nch / (ncu - cus))
+        key = (round(period, 9), k, cus)
+        if best is None or key < best[0]:
+            best = (key, cus)
     return best[1] if best else 64
 
 
@@ -194,7 +196,9 @@ class GpuStepper:
         # post streams the complement, so that no other kernel shares a CU's issue slots with the
         # PLL's waves (profiles/r01/ab_cumask.txt). Default: pll_cus(nch).
         self.created: list[int] = []
-        cu_spec = os.environ.get("SDR_BENCH_CUMASK", str(pll_cus(nch)))
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        cu_spec = os.environ.get("SDR_BENCH_CUMASK") or str(
+            pll_cus(nch, lambda n: self.pipe.plls_fits(n)["fits"], ncu))
         if cu_spec not in ("", "0"):
             try:
                 # the all-CU fill/drain stream is a fourth dedicated hardware queue: at N > 1 RCCL's

@@ -195,8 +195,11 @@ int sdr_plls(sdr_ctx *ctx, void *stream);
  * waits for each block's signal (a device flag written in stream order), runs both PLLs, and
  * releases the waiting stream. The PLL stream must be one sdr_stream_create_cu_range made (it owns
  * its hardware queue; on a pool stream a signal could queue behind the waiting launch), and every
- * wave of the launch must fit that stream's CUs at once: otherwise the launch is refused with
- * SDR_E_INVALID before anything is dispatched (use sdr_plls). A wait longer than 5 s (a block
+ * workgroup of the launch must be resident on that stream's CUs at once -- by the workgroups of its
+ * kernel that fit one CU and by how the CU mask falls on the XCCs' shader engines (workgroups are
+ * dealt to the engines evenly, so an engine with fewer CUs of the mask fills first; sdr_plls_fits):
+ * otherwise the launch is refused with SDR_E_INVALID before anything is enqueued (use sdr_plls, or
+ * another CU range). A wait longer than 5 s (a block
  * never signalled, or a post stream that waits for a block the PLL never finished) ends the launch
  * without computing: from then on the post stages of that launch's blocks write SDR_PCM_POISON
  * audio, NaN rds_clean rows and nbits = SDR_NBITS_POISONED (never audio from phases the PLL did
@@ -210,6 +213,10 @@ int sdr_plls(sdr_ctx *ctx, void *stream);
  * again while blocks of the previous launch were never signalled first lets that launch time out
  * and drain. Not with SDR_FLAG_PLL_LIBM. */
 int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
+/* Would sdr_plls_launch accept a stream made by sdr_stream_create_cu_range(first_cu, n_cu, exclude
+ * = 0) for this context? Fills the launch's waves, its workgroups and how many of them that CU range
+ * keeps resident at once; it fits when *groups <= *resident. No stream is made, nothing is enqueued. */
+int sdr_plls_fits(sdr_ctx *ctx, int first_cu, int n_cu, int *waves, long long *groups, long long *resident);
 /* Optional, ahead of sdr_plls_launch(nblocks) (e.g. before a timed region): the launch's
  * bookkeeping -- allocation, the reset of its stamps and error word -- in `stream`'s order, so the
  * launch itself only enqueues the kernel. Ignored by a launch with another nblocks. */

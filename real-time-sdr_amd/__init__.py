@@ -100,6 +100,7 @@ def lib() -> C.CDLL:
         "sdr_plls": ([vp, vp], i32),
         "sdr_plls_launch": ([vp, i32, vp], i32),
         "sdr_plls_prepare": ([vp, i32, vp], i32),
+        "sdr_plls_fits": ([vp, i32, i32, C.POINTER(i32), C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)], i32),
         "sdr_plls_signal": ([vp, vp], i32),
         "sdr_frontend_pre_parts": ([vp, vp, sz, i32, vp], i32),
         "sdr_plls_wait": ([vp, vp], i32),
@@ -360,6 +361,13 @@ class Pipeline:
     # persistent PLLs (include/sdr_amd.h): one dispatch for many blocks
     def plls_launch(self, nblocks: int, stream=None):
         check(lib().sdr_plls_launch(self._h, nblocks, _stream(stream)), "sdr_plls_launch")
+
+    def plls_fits(self, n_cu: int, first_cu: int = 0) -> dict:
+        """Would plls_launch accept a stream over CUs [first_cu, first_cu + n_cu)? The launch's waves,
+        workgroups and how many of those the range keeps resident at once (sdr_plls_fits)."""
+        w, g, r = C.c_int(), C.c_longlong(), C.c_longlong()
+        check(lib().sdr_plls_fits(self._h, first_cu, n_cu, C.byref(w), C.byref(g), C.byref(r)), "sdr_plls_fits")
+        return {"waves": w.value, "groups": g.value, "resident": r.value, "fits": g.value <= r.value}
 
     def plls_prepare(self, nblocks: int, stream=None):
         """The launch's bookkeeping ahead of plls_launch(nblocks) (allocation, stamp reset)."""

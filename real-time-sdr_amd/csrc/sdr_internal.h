@@ -126,9 +126,35 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
 // done[s % PLL_DONE_RING] reaches waves * (s / PLL_DONE_RING + 1): per-block counters, because
 // waves drift apart by more than a block (a wave that redoes many chunks lags the others, which
 // may already finish the next block) and one shared count would release a block early.
+// What a CU mask holds at once (tools/microbench/cumask_probe.hip, profiles/r06/cumask/): bit b of a
+// HIP CU mask is CU slot j = b / NXCC of XCC b % NXCC, and slot j sits in shader engine j % 4 of that
+// XCC (4 SEs x 8 CUs per XCC on MI355X). Workgroups are dealt round-robin over the XCCs and, inside
+// one, over its SEs whether or not the SE has room, so a launch is resident at once only while every
+// SE's share fits its CUs: a 48-CU mask gives each XCC SEs of 2, 2, 1 and 1 CUs, and 96 workgroups at
+// two per CU left 32 of them waiting (the 1536-channel timeout of round 5). Measured bound, never
+// exceeded over 1, 2 and 4 workgroups per CU and masks of 8..192 CUs:
+//   resident workgroups <= xcc_active x min over those XCCs of (SEs with CUs x min CUs per such SE) x per_cu
+struct CuPlacement {
+    int ncu = 0;            // CUs in the mask
+    int xcc_active = 0;     // XCCs with a CU in the mask
+    int min_units = 0;      // min over active XCCs of (active SEs x min CUs per active SE)
+    long long resident(int per_cu) const { return (long long)xcc_active * min_units * per_cu; }
+};
+CuPlacement cu_placement(const uint32_t* mask, int nwords, int ncu_dev, int nxcc);
+// the persistent PLL launch's shape for these jobs: kernel, workgroups, waves, and how many of its
+// workgroups the placement keeps resident at once (resident < groups: the launch would hang)
+struct PllMultiPlan {
+    const void* kern = nullptr;
+    int WG = 1, tab_ok = 0, per_cu = 0;
+    size_t lds = 0;
+    dim3 g, b;
+    uint32_t waves = 0;
+    long long groups = 0, resident = 0;
+};
+int pll_multi_plan(const PllJobs2& jobs, int n, int nch, const CuPlacement& pl, PllMultiPlan* plan);
 int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
-                     hipStream_t s, int max_cus,    // max_cus > 0: fail unless every wave fits max_cus CUs
+                     hipStream_t s, const CuPlacement& pl,   // refused unless every workgroup is resident at once
                      int sub_tile);                 // > 0: the first block's input may come in parts of this many samples
 int launch_flag_store(uint32_t* flag, uint32_t v, hipStream_t s);
 int launch_flag_wait(const uint32_t* ctr, uint32_t want, uint32_t* err, hipStream_t s);

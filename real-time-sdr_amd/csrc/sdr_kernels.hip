@@ -84,6 +84,17 @@ __device__ __forceinline__ uint32_t poison_word(const Poison& p) {
     if (p.fail) v |= *p.fail;
     return __builtin_amdgcn_readfirstlane(v);
 }
+// The same words read again once the kernel's input loads have completed (issued after the staging
+// barrier, consumed before the stores, so its latency hides behind the compute): a release wait that
+// expires while a reader runs sets its word before the producer overwrites that reader's inputs, so
+// a reader that loaded any overwritten sample sees the word here (agent-scope loads: from L2, the
+// coherence point) and poisons instead of storing a mixed block.
+__device__ __forceinline__ uint32_t poison_late(const Poison& p) {
+    uint32_t v = 0;
+    if (p.pers) v |= __hip_atomic_load(p.pers, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p.fail) v |= __hip_atomic_load(p.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
 
 // ------------------------------------------------------------------------------------------
 // Decimating FIR, filter.cpp:106-121: y[n] = sum_{k<ntaps} h[k] * x[nD-k], ascending k, f32
@@ -208,6 +219,7 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
     __syncthreads();
     const int nb = n0 + tid * R;
     if (nb >= ny) return;
+    const uint32_t late = checks ? poison_late(f.err) : 0u;     // after every input load of the tile
     // w[i] = x[nb - (T-1) + i]; output nb + j at tap k reads w[j + T-1 - k] (samples past the
     // staged window only feed outputs >= ny, which are not stored)
     float w[R + T - 1 + 3];
@@ -327,7 +339,7 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
     for (int t = 0; t < NT; t++)
 #pragma unroll
         for (int j = 0; j < R; j++) asm volatile("" : "+v"(a[t][j]));
-    if (checks && s_poison != 0u) {                               // no valid input behind this block
+    if (checks && (s_poison | __builtin_amdgcn_readfirstlane(late)) != 0u) {   // no valid input behind this block
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
@@ -842,12 +854,14 @@ __global__ __launch_bounds__(AT) void k_mono_out(const float* __restrict__ fm, s
             if (ob + r < ny) o[r] = SDR_PCM_POISON;
         return;
     }
+    const uint32_t late = poison_late(err);                  // after every input load of the tile
     float w[TW], acc[AR];
     audio_window<D>(sa, tid, w);
     audio_mac<D>(h, w, acc);
+    const bool bad = __builtin_amdgcn_readfirstlane(late) != 0u;
 #pragma unroll
     for (int r = 0; r < AR; r++)
-        if (ob + r < ny) o[r] = cvt_i16_x86(16384 * acc[r]);   // mono.cpp:41
+        if (ob + r < ny) o[r] = bad ? (int16_t)SDR_PCM_POISON : cvt_i16_x86(16384 * acc[r]);   // mono.cpp:41
 }
 
 // ------------------------------------------------------------------------------------------
@@ -943,17 +957,19 @@ __global__ __launch_bounds__(AT) void k_stereo_out(const StereoOut a) {
             if (ob + r < a.ny) o[r] = pp;
         return;
     }
+    const uint32_t late = poison_late(a.err);                      // after every input load of the tile
     float w[TW], m[AR], sv[AR];
     audio_window<D>(sa, tid, w);
     audio_mac<D>(a.h, w, m);                                       // mono resampler (:94)
     audio_window<D>(sb, tid, w);
     audio_mac<D>(a.h, w, sv);                                      // stereo resampler (:97)
+    const bool bad = __builtin_amdgcn_readfirstlane(late) != 0u;
 #pragma unroll
     for (int r = 0; r < AR; r++) {
         if (ob + r < a.ny) {
             const uint16_t l = (uint16_t)cvt_i16_x86(16384 * (m[r] + sv[r]));   // stereo.cpp:100-102
             const uint16_t rr = (uint16_t)cvt_i16_x86(16384 * (m[r] - sv[r]));
-            o[r] = (uint32_t)l | ((uint32_t)rr << 16);
+            o[r] = bad ? (uint32_t)(uint16_t)SDR_PCM_POISON * 0x10001u : (uint32_t)l | ((uint32_t)rr << 16);
         }
     }
 }
@@ -1555,28 +1571,84 @@ int release_stream_scratch(hipStream_t s) {
     return SDR_OK;
 }
 
-// Streams made by sdr_stream_create_cu_range, with their device and CU count. The persistent PLL
-// launch accepts only these: each has its own hardware queue (a pool stream can share one with the
-// stream that signals the blocks, which then never runs), and its CU count bounds how many of the
-// launch's waves can be resident at once.
+// Streams made by sdr_stream_create_cu_range, with their device, CU mask and placement. The
+// persistent PLL launch accepts only these: each has its own hardware queue (a pool stream can share
+// one with the stream that signals the blocks, which then never runs), and its mask's placement
+// bounds how many of the launch's workgroups can be resident at once (sdr_internal.h CuPlacement).
 struct MaskedStream {
     hipStream_t s;
-    int device, ncu;
+    int device;
+    CuPlacement place;
 };
 std::mutex g_masked_mu;
 std::vector<MaskedStream> g_masked;
 
-bool masked_stream(hipStream_t s, int* device, int* ncu) {
+bool masked_stream(hipStream_t s, int* device, CuPlacement* place) {
     std::lock_guard<std::mutex> lk(g_masked_mu);
     for (const MaskedStream& m : g_masked)
         if (m.s == s && s != nullptr) {
             *device = m.device;
-            *ncu = m.ncu;
+            if (place) *place = m.place;
             return true;
         }
     return false;
 }
 
+// the mask of CUs [first_cu, first_cu + n_cu) of a device (or of every other CU: exclude)
+std::vector<uint32_t> cu_range_mask(int ncu, int first_cu, int n_cu, int exclude, int* nset) {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    *nset = 0;
+    for (int cu = 0; cu < ncu; ++cu) {
+        const bool in = cu >= first_cu && cu < first_cu + n_cu;
+        if (in != (exclude != 0)) {
+            mask[cu / 32] |= 1u << (cu % 32);
+            ++*nset;
+        }
+    }
+    return mask;
+}
+
+int device_xccs(int device) {
+    int nx = 0;
+    if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, device) != hipSuccess || nx <= 0) nx = 8;
+    return nx;
+}
+
+}  // namespace
+
+CuPlacement sdrk::cu_placement(const uint32_t* mask, int nwords, int ncu_dev, int nxcc) {
+    constexpr int SE_PER_XCC = 4;   // MI355X: 32 shader engines over 8 XCCs
+    CuPlacement pl;
+    if (nxcc <= 0 || ncu_dev % nxcc) nxcc = 1;
+    const int slots = ncu_dev / nxcc;
+    int min_units = -1;
+    for (int x = 0; x < nxcc; x++) {
+        int per_se[SE_PER_XCC] = {};
+        int nx = 0;
+        for (int j = 0; j < slots; j++) {
+            const int bit = j * nxcc + x;
+            if (bit / 32 < nwords && (mask[bit / 32] >> (bit % 32) & 1u)) {
+                per_se[j % SE_PER_XCC]++;
+                nx++;
+            }
+        }
+        pl.ncu += nx;
+        if (!nx) continue;
+        pl.xcc_active++;
+        int active = 0, lo = slots;
+        for (int k = 0; k < SE_PER_XCC; k++)
+            if (per_se[k]) {
+                active++;
+                lo = std::min(lo, per_se[k]);
+            }
+        const int units = active * lo;
+        min_units = min_units < 0 ? units : std::min(min_units, units);
+    }
+    pl.min_units = std::max(min_units, 0);
+    return pl;
+}
+
+namespace {
 }  // namespace
 
 extern "C" {
@@ -1599,20 +1671,13 @@ int sdr_stream_create_cu_range(void** stream, int device, int first_cu, int n_cu
     if (first_cu < 0 || n_cu <= 0 || first_cu + n_cu > ncu || (exclude && n_cu >= ncu))
         return fail(SDR_E_INVALID, "sdr_stream_create_cu_range: CUs [%d, %d) outside [0, %d)",
                     first_cu, first_cu + n_cu, ncu);
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
     int nset = 0;
-    for (int cu = 0; cu < ncu; ++cu) {
-        const bool in = cu >= first_cu && cu < first_cu + n_cu;
-        if (in != (exclude != 0)) {
-            mask[cu / 32] |= 1u << (cu % 32);
-            nset++;
-        }
-    }
+    std::vector<uint32_t> mask = cu_range_mask(ncu, first_cu, n_cu, exclude, &nset);
     hipStream_t s = nullptr;
     HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
     {
         std::lock_guard<std::mutex> lk(g_masked_mu);
-        g_masked.push_back(MaskedStream{s, device, nset});
+        g_masked.push_back(MaskedStream{s, device, cu_placement(mask.data(), (int)mask.size(), ncu, device_xccs(device))});
     }
     *stream = s;
     return SDR_OK;
@@ -1952,6 +2017,28 @@ int check_failed(const sdr_ctx* c, const char* what) {
 }
 // the error words of the current block's output stages (kernel side: Poison)
 Poison block_poison(const sdr_ctx* c) { return Poison{c->pers_err(), c->fail_words}; }
+// After a stage that read the persistent launch's error word was enqueued on `s`: record that
+// stream's reader event now, so the next launch's prepare can order its reset of the word after
+// every reader by waiting on the events alone -- no stream handle is used after the call that
+// supplied it (the handle only names the event's slot; a stream destroyed since is never touched).
+// More than PERS_READERS streams fall back to a device synchronisation in the prepare.
+int pers_reader_mark(sdr_ctx* c, hipStream_t s) {
+    if (!c->pers_err()) return SDR_OK;
+    int slot = -1;
+    for (int i = 0; i < c->pers_nreaders && i < sdr_ctx::PERS_READERS; i++)
+        if (c->pers_readers[i] == s) slot = i;
+    if (slot < 0) {
+        if (c->pers_nreaders >= sdr_ctx::PERS_READERS) {
+            c->pers_nreaders = sdr_ctx::PERS_READERS + 1;
+            return SDR_OK;
+        }
+        slot = c->pers_nreaders++;
+        c->pers_readers[slot] = s;
+    }
+    if (!c->pers_reader_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&c->pers_reader_ev[slot], hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->pers_reader_ev[slot], s));
+    return SDR_OK;
+}
 int check_iq(const sdr_ctx* c, const uint8_t* iq, size_t iq_stride) {
     const sdr_info& in = c->info;
     if (iq_stride < (size_t)2 * in.block_iq || (iq_stride & 1) || (reinterpret_cast<uintptr_t>(iq) & 1))
@@ -2100,6 +2187,7 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
                                in.n_audio, audio, audio_stride, block_poison(c));
         LAUNCH_CHECK();
         c->mono_done = c->block;
+        if (const int r = pers_reader_mark(c, S(stream))) return r;
         return release_record(c, REL_MONO, S(stream));
     }
     const int tile = 512;
@@ -2114,6 +2202,7 @@ int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
                        audio, audio_stride, in.n_audio);
     LAUNCH_CHECK();
     c->mono_done = c->block;
+    if (const int r = pers_reader_mark(c, S(stream))) return r;
     return release_record(c, REL_MONO, S(stream));
 }
 
@@ -2238,6 +2327,7 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
             hipLaunchKernelGGL(k_stereo_out<9>, g, dim3(AT), 0, s, a);
         LAUNCH_CHECK();
         c->stereo_done = c->block;
+        if (const int r = pers_reader_mark(c, s)) return r;
         return release_record(c, REL_STEREO, s);
     }
     {
@@ -2267,6 +2357,7 @@ int sdr_stereo_post(sdr_ctx* c, int16_t* lr, size_t lr_stride, void* stream) {
                        lr_stride, 2 * in.n_audio);
     LAUNCH_CHECK();
     c->stereo_done = c->block;
+    if (const int r = pers_reader_mark(c, s)) return r;
     return release_record(c, REL_STEREO, s);
 }
 
@@ -2384,7 +2475,7 @@ int sdr_plls(sdr_ctx* c, void* stream) {
 // the bookkeeping of a persistent launch: recover an abandoned previous launch, allocate the words
 // and stamp arrays, reset this launch's stamps and error word (stream order on `stream`)
 static int plls_prepare(sdr_ctx* c, int nblocks, hipStream_t s) {
-    int dev_unused = 0, ncu_unused = 0;
+    int dev_unused = 0;
     if (c->pers_signaled != c->pers_launched) {
         // blocks of the previous launch were never signalled: its waves give up on them after the
         // bounded wait (PLL_WAIT_TICKS) and still count them done. Let it drain, then resynchronise
@@ -2393,7 +2484,7 @@ static int plls_prepare(sdr_ctx* c, int nblocks, hipStream_t s) {
         c->pers_signaled = c->pers_waited = c->pers_launched;
         HIP_TRY(hipMemcpyAsync(c->pers_words, &c->pers_launched, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     } else if (c->pers_stream && c->pers_stream != s && c->pers_launched != 0 &&
-               masked_stream(c->pers_stream, &dev_unused, &ncu_unused)) {
+               masked_stream(c->pers_stream, &dev_unused, nullptr)) {
         // every block of the previous launch is signalled, but its waves may still be stamping its
         // last blocks or setting its error word: the resets below wait for that launch in `s`'s order
         // (a PLL stream destroyed since has completed its work: hipStreamDestroy waits for it)
@@ -2434,12 +2525,8 @@ static int plls_prepare(sdr_ctx* c, int nblocks, hipStream_t s) {
     if (c->pers_nreaders > sdr_ctx::PERS_READERS) {
         HIP_TRY(hipDeviceSynchronize());
     } else {
-        for (int i = 0; i < c->pers_nreaders; i++) {
-            if (c->pers_readers[i] == s) continue;
-            if (!c->pers_reader_ev[i]) HIP_TRY(hipEventCreateWithFlags(&c->pers_reader_ev[i], hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(c->pers_reader_ev[i], c->pers_readers[i]));
-            HIP_TRY(hipStreamWaitEvent(s, c->pers_reader_ev[i], 0));
-        }
+        for (int i = 0; i < c->pers_nreaders; i++)   // recorded by the readers (pers_reader_mark)
+            if (c->pers_reader_ev[i]) HIP_TRY(hipStreamWaitEvent(s, c->pers_reader_ev[i], 0));
     }
     c->pers_nreaders = 0;
     HIP_TRY(hipMemsetAsync(c->pers_words + 1, 0, sizeof(uint32_t), s));
@@ -2455,32 +2542,11 @@ int sdr_plls_prepare(sdr_ctx* c, int nblocks, void* stream) {
     return plls_prepare(c, nblocks, S(stream));
 }
 
-int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
-    if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_launch: bad arguments");
-    if (const int rf_ = check_failed(c, "plls_launch")) return rf_;
-    if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_launch: not with SDR_FLAG_PLL_LIBM");
-    hipStream_t s = S(stream);
-    // the launch's waves spin until later dispatches on other streams publish each block, so the
-    // PLL stream must own its hardware queue (pool streams share GPU_MAX_HW_QUEUES queues with the
-    // streams that signal) and every wave must fit the stream's CUs at once: refused before any
-    // dispatch otherwise (a waiting launch could never finish, and its blocks would time out)
-    int sdev = -1, scus = 0;
-    if (!masked_stream(s, &sdev, &scus))
-        return fail(SDR_E_INVALID, "plls_launch: the PLL stream was not made by sdr_stream_create_cu_range (a "
-                                   "persistent launch needs a stream with its own hardware queue; use sdr_plls)");
-    if (sdev != c->device)
-        return fail(SDR_E_INVALID, "plls_launch: the PLL stream is on device %d, the context on %d", sdev, c->device);
-    HIP_TRY(hipSetDevice(c->device));
-    // prepared ahead (sdr_plls_prepare, same nblocks, no launch since): only the launch is left
-    if (!(c->pers_prepared == nblocks && c->pers_prepared_launch == c->pers_launched &&
-          c->pers_signaled == c->pers_launched)) {
-        const int r = plls_prepare(c, nblocks, s);
-        if (r) return r;
-    }
-    c->pers_prepared = 0;
-    const int n = c->info.block_if, nch = c->nch;
+// the persistent launch's jobs: both PLLs of the two parities, p[0] = the parity the next
+// sdr_frontend switches to
+static PllJobs2 plls_jobs(sdr_ctx* c) {
     PllJobs2 jobs{};
-    const int first_parity = c->parity ^ 1;   // the parity the next sdr_frontend switches to: p[0]
+    const int first_parity = c->parity ^ 1;
     for (int k = 0; k < 2; k++) {
         const int saved = c->parity;
         c->parity = first_parity ^ k;
@@ -2488,9 +2554,67 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
         jobs.p[k].j[1] = rds_job(c);
         c->parity = saved;
     }
+    return jobs;
+}
+
+int sdr_plls_fits(sdr_ctx* c, int first_cu, int n_cu, int* waves, long long* groups, long long* resident) {
+    if (!c || !waves || !groups || !resident) return fail(SDR_E_INVALID, "plls_fits: bad arguments");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, c->device));
+    const int ncu = prop.multiProcessorCount;
+    if (first_cu < 0 || n_cu <= 0 || first_cu + n_cu > ncu)
+        return fail(SDR_E_INVALID, "plls_fits: CUs [%d, %d) outside [0, %d)", first_cu, first_cu + n_cu, ncu);
+    int nset = 0;
+    const std::vector<uint32_t> mask = cu_range_mask(ncu, first_cu, n_cu, 0, &nset);
+    const CuPlacement pl = cu_placement(mask.data(), (int)mask.size(), ncu, device_xccs(c->device));
+    HIP_TRY(hipSetDevice(c->device));
+    PllMultiPlan P;
+    if (const int r = pll_multi_plan(plls_jobs(c), c->info.block_if, c->nch, pl, &P)) return r;
+    *waves = (int)P.waves;
+    *groups = P.groups;
+    *resident = P.resident;
+    return SDR_OK;
+}
+
+int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
+    if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_launch: bad arguments");
+    if (const int rf_ = check_failed(c, "plls_launch")) return rf_;
+    if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_launch: not with SDR_FLAG_PLL_LIBM");
+    hipStream_t s = S(stream);
+    // the launch's waves spin until later dispatches on other streams publish each block, so the
+    // PLL stream must own its hardware queue (pool streams share GPU_MAX_HW_QUEUES queues with the
+    // streams that signal) and every workgroup must be resident on the stream's CUs at once: refused
+    // before anything is enqueued otherwise (a waiting launch could never finish, and its blocks would
+    // time out)
+    int sdev = -1;
+    CuPlacement pl;
+    if (!masked_stream(s, &sdev, &pl))
+        return fail(SDR_E_INVALID, "plls_launch: the PLL stream was not made by sdr_stream_create_cu_range (a "
+                                   "persistent launch needs a stream with its own hardware queue; use sdr_plls)");
+    if (sdev != c->device)
+        return fail(SDR_E_INVALID, "plls_launch: the PLL stream is on device %d, the context on %d", sdev, c->device);
+    HIP_TRY(hipSetDevice(c->device));
+    const int n = c->info.block_if, nch = c->nch;
+    const PllJobs2 jobs = plls_jobs(c);
+    {
+        PllMultiPlan P;
+        if (const int r = pll_multi_plan(jobs, n, nch, pl, &P)) return r;
+        if (P.groups > P.resident)
+            return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit the stream's %d CUs: %lld of %lld workgroups "
+                        "of %d waves resident at once (%d per CU, %d XCCs x %d SE-balanced CU slots; use sdr_plls, "
+                        "a stream over more CUs, or sdr_plls_fits to pick one)", P.waves, pl.ncu, P.resident,
+                        P.groups, P.WG, P.per_cu, pl.xcc_active, pl.min_units);
+    }
+    // prepared ahead (sdr_plls_prepare, same nblocks, no launch since): only the launch is left
+    if (!(c->pers_prepared == nblocks && c->pers_prepared_launch == c->pers_launched &&
+          c->pers_signaled == c->pers_launched)) {
+        const int r = plls_prepare(c, nblocks, s);
+        if (r) return r;
+    }
+    c->pers_prepared = 0;
     uint32_t waves = 0;
     const int r = launch_pll_multi(jobs, n, nch, nblocks, c->pers_words, c->pers_launched, c->pers_t0, c->pers_t1,
-                                   c->pers_cyc, &waves, s, scus, FRB_TILE);
+                                   c->pers_cyc, &waves, s, pl, FRB_TILE);
     if (r) return r;
     c->pers_failed = false;   // this launch's error word was cleared by its prepare
     c->pers_waves = waves;
@@ -2594,13 +2718,9 @@ int sdr_plls_wait(sdr_ctx* c, void* stream) {
     // them (a post stream not in the list -- more than PERS_READERS of them -- falls back to a device
     // synchronisation there)
     hipStream_t ws = S(stream);
-    bool known = false;
-    for (int i = 0; i < c->pers_nreaders; i++) known |= c->pers_readers[i] == ws;
-    if (!known) {
-        if (c->pers_nreaders < sdr_ctx::PERS_READERS) c->pers_readers[c->pers_nreaders++] = ws;
-        else c->pers_nreaders = sdr_ctx::PERS_READERS + 1;   // overflow: synchronise in the prepare
-    }
-    return launch_flag_wait(c->pers_words + PLL_WORDS_DONE + seq % PLL_DONE_RING, want, c->pers_words + 1, S(stream));
+    if (const int r = launch_flag_wait(c->pers_words + PLL_WORDS_DONE + seq % PLL_DONE_RING, want, c->pers_words + 1, ws))
+        return r;
+    return pers_reader_mark(c, ws);
 }
 
 int sdr_plls_report(sdr_ctx* c, double* block_ms, int max_blocks, int* nblocks, void* stream) {
@@ -2738,7 +2858,7 @@ int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) 
         if (r) return r;
     }
     c->rds_dsp_done = c->block;
-    return SDR_OK;
+    return pers_reader_mark(c, s);
 }
 
 int sdr_rds_dsp(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
@@ -2765,7 +2885,7 @@ int sdr_rds_bits(sdr_ctx* c, int32_t* offset, int32_t* nsym, uint8_t* symbols, s
                        (reinterpret_cast<uintptr_t>(c->rds_clean) % 16 == 0 && c->clean_stride % 4 == 0) ? 1 : 0);
     LAUNCH_CHECK();
     c->rds_bits_done = c->block;
-    return SDR_OK;
+    return pers_reader_mark(c, S(stream));
 }
 
 int sdr_ctx_buffer(sdr_ctx* c, const char* name, const float** ptr, size_t* stride, int* len) {

@@ -751,9 +751,11 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
 // line-shaped pieces out). The
 // one-wave-per-CU path (the headline) keeps the register prefetch, which needs no LDS round trip.
 // Layout of one buffer: pieces of 1 KiB at a 1040-byte pitch (a 16-byte rotation per piece keeps
-// the own-row reads free of bank conflicts): pieces 0-1 hold the x rows of channels q with q % 2 = k
-// (lane A, which runs on -x, flips the sign bit as it reads), pieces 4-7 the rx rows q with
-// q % 4 = k. Every lane of the wave must run the loop (all 32 channels valid).
+// the own-row reads free of bank conflicts): 6 pieces per buffer (COAL_BUF), pieces 0-1 the x rows of
+// channels q with q % 2 = k (lane A, which runs on -x, flips the sign bit as it reads), pieces 2-5 the
+// rx rows q with q % 4 = k (piece 2 + k); a ring of COAL_RING = 3 buffers per wave, so a chunk's 6
+// DMA pieces are in flight while the own-row reads wait for the older chunk's (vmcnt(6)). Every lane
+// of the wave must run the loop (all 32 channels valid).
 // ------------------------------------------------------------------------------------------
 constexpr int COAL_PIECE = 1040;
 constexpr int COAL_BUF = 6 * COAL_PIECE;              // pieces 0-1: x rows, 2-5: rx rows
@@ -1000,7 +1002,8 @@ __global__ __launch_bounds__(64 * WG) void k_pll_multi(const PllJobs2 jobs, int 
     extern __shared__ double wtab[];
     __shared__ double sh_toff;
     __shared__ int sh_dead;
-    // COAL: per wave two DMA buffers and the phase staging rows (pll_run_split_coal)
+    // COAL: per wave a ring of COAL_RING (3) DMA buffers of 6 pieces and the phase staging rows
+    // (pll_run_split_coal)
     __shared__ __attribute__((aligned(16))) uint8_t coal_buf[COAL ? WG * COAL_RING * COAL_BUF : 16];
     __shared__ __attribute__((aligned(16))) uint8_t coal_tst[COAL ? WG * 32 * COAL_TROW : 16];
     uint8_t* const my_buf = coal_buf + (COAL ? (threadIdx.x >> 6) * COAL_RING * COAL_BUF : 0);
@@ -1300,9 +1303,7 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
     return launch_plls(libm, jobs, 1, n, nch, s);
 }
 
-int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
-                     unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
-                     hipStream_t s, int max_cus, int sub_tile) {
+int pll_multi_plan(const PllJobs2& jobs, int n, int nch, const CuPlacement& pl, PllMultiPlan* plan) {
     bool vec = true, split = true;
     for (int k = 0; k < 2; k++)
         for (int q = 0; q < 2; q++) {
@@ -1313,20 +1314,18 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
                   (!j.in_neg || (reinterpret_cast<uintptr_t>(j.in_neg) % 16 == 0 && j.neg_stride % 4 == 0));
             split = split && j.in_neg;
         }
+    PllMultiPlan& P = *plan;
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
-    const int tab_ok = tab_bytes <= 64 * 1024 ? 1 : 0;
-    const size_t lds = tab_ok ? tab_bytes : 0;
+    P.tab_ok = tab_bytes <= 64 * 1024 ? 1 : 0;
+    P.lds = P.tab_ok ? tab_bytes : 0;
     const int wave_cnt = cdiv(split ? 2 * nch : nch, 64) * 2;
     // one wave per workgroup (its own CU time slice and table) while two tables per CU fit the
     // stream's CUs, else groups of 4 waves -- one per SIMD -- sharing one table per CU
-    const int WG = (max_cus > 0 && wave_cnt > 2 * max_cus) ? 4 : 1;
-    const dim3 g(cdiv(split ? 2 * nch : nch, 64 * WG), 2), b(64 * WG);
-    *waves = g.x * g.y * WG;
-    // packed groups (more than two waves per CU): the chunk inputs and phases through LDS in
-    // line-shaped pieces (pll_run_split_coal; every lane of every wave must hold a channel): 357 -> 262
-    // cycles per step at four waves per CU; at two it measured 231-235 -> 237, so one-wave groups keep
-    // the register prefetch (profiles/r05/coal/)
-    const bool coal = vec && split && nch % 32 == 0 && WG == 4;
+    P.WG = wave_cnt > 2 * pl.ncu ? 4 : 1;
+    P.g = dim3(cdiv(split ? 2 * nch : nch, 64 * P.WG), 2);
+    P.b = dim3(64 * P.WG);
+    P.waves = P.g.x * P.g.y * P.WG;
+    P.groups = (long long)P.g.x * P.g.y;
     auto kern_of = [&](auto v, auto sp, auto wg) -> const void* {
         return reinterpret_cast<const void*>(k_pll_multi<decltype(v)::value, decltype(sp)::value, decltype(wg)::value>);
     };
@@ -1334,27 +1333,58 @@ int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t
     using F = std::false_type;
     using W1 = std::integral_constant<int, 1>;
     using W4 = std::integral_constant<int, 4>;
-    const void* kern = coal ? reinterpret_cast<const void*>(k_pll_multi<true, true, 4, true>)
-                     : WG == 4 ? (vec ? (split ? kern_of(T{}, T{}, W4{}) : kern_of(T{}, F{}, W4{}))
-                                      : (split ? kern_of(F{}, T{}, W4{}) : kern_of(F{}, F{}, W4{})))
-                               : (vec ? (split ? kern_of(T{}, T{}, W1{}) : kern_of(T{}, F{}, W1{}))
-                                      : (split ? kern_of(F{}, T{}, W1{}) : kern_of(F{}, F{}, W1{})));
-    // every wave of a persistent launch must be resident at once (a wave that cannot start holds up
-    // the done count of every block, and the producer of later blocks waits for that): at most the
-    // stream's CUs x the workgroups of this kernel that fit one CU (its VGPRs, the LDS table)
-    if (max_cus > 0) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WG, lds) != hipSuccess || per_cu <= 0)
-            per_cu = std::min(4 / WG, tab_ok ? (int)(160 * 1024 / tab_bytes) : 4 / WG);
-        if ((long long)g.x * g.y > (long long)max_cus * per_cu)
-            return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit the stream's %d CUs x %d resident waves "
-                        "(use sdr_plls, or a stream over more CUs)", *waves, max_cus, per_cu * WG);
+    const void* plain = P.WG == 4 ? (vec ? (split ? kern_of(T{}, T{}, W4{}) : kern_of(T{}, F{}, W4{}))
+                                         : (split ? kern_of(F{}, T{}, W4{}) : kern_of(F{}, F{}, W4{})))
+                                  : (vec ? (split ? kern_of(T{}, T{}, W1{}) : kern_of(T{}, F{}, W1{}))
+                                         : (split ? kern_of(F{}, T{}, W1{}) : kern_of(F{}, F{}, W1{})));
+    // every workgroup of a persistent launch must be resident at once (a wave that cannot start holds
+    // up the done count of every block, and the producer of later blocks waits for that): the
+    // workgroups of this kernel that fit one CU (its VGPRs, the LDS table) times what the placement of
+    // the stream's CU mask keeps resident (sdr_internal.h CuPlacement)
+    auto resident = [&](const void* kern, int* per_cu) {
+        *per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, kern, 64 * P.WG, P.lds) != hipSuccess || *per_cu <= 0)
+            *per_cu = std::min(4 / P.WG, P.tab_ok ? (int)(160 * 1024 / tab_bytes) : 4 / P.WG);
+        return pl.resident(*per_cu);
+    };
+    // packed groups (more than two waves per CU): the chunk inputs and phases through LDS in
+    // line-shaped pieces (pll_run_split_coal; every lane of every wave must hold a channel): 357 -> 262
+    // cycles per step at four waves per CU; at two it measured 231-235 -> 237, so one-wave groups keep
+    // the register prefetch (profiles/r05/coal/). Its staging ring (3 x 6 KiB + 2.5 KiB per wave, 83 KiB per
+    // group, beside the table) fits one group per CU: a launch that needs more falls back to the register-prefetch
+    // groups, which fit two.
+    P.kern = plain;
+    if (vec && split && nch % 32 == 0 && P.WG == 4) {
+        const void* coal = reinterpret_cast<const void*>(k_pll_multi<true, true, 4, true>);
+        int pc = 0;
+        const long long r = resident(coal, &pc);
+        if (r >= P.groups) {
+            P.kern = coal;
+            P.per_cu = pc;
+            P.resident = r;
+            return SDR_OK;
+        }
     }
+    P.resident = resident(plain, &P.per_cu);
+    return SDR_OK;
+}
+
+int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
+                     unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
+                     hipStream_t s, const CuPlacement& pl, int sub_tile) {
+    PllMultiPlan P;
+    if (const int r = pll_multi_plan(jobs, n, nch, pl, &P)) return r;
+    *waves = P.waves;
+    if (P.groups > P.resident)
+        return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit the stream's %d CUs: %lld of %lld workgroups of "
+                    "%d waves resident at once (%d per CU, %d XCCs x %d SE-balanced CU slots; use sdr_plls, a "
+                    "stream over more CUs, or sdr_plls_fits to pick one)", P.waves, pl.ncu, P.resident, P.groups,
+                    P.WG, P.per_cu, pl.xcc_active, pl.min_units);
     hipLaunchKernelGGL(reinterpret_cast<void (*)(PllJobs2, int, int, int, int, const uint32_t*, uint32_t, uint32_t*,
                                                  uint32_t*, unsigned long long*, unsigned long long*,
                                                  unsigned long long*, const uint32_t*, uint32_t, int)>(
-                           const_cast<void*>(kern)),
-                       g, b, lds, s, jobs, n, nch, tab_ok, nblocks, words, pre_first, words + PLL_WORDS_DONE,
+                           const_cast<void*>(P.kern)),
+                       P.g, P.b, P.lds, s, jobs, n, nch, P.tab_ok, nblocks, words, pre_first, words + PLL_WORDS_DONE,
                        words + 1, t0, t1, tc, sub_tile > 0 ? words + PLL_WORD_SUB : nullptr,
                        pre_first * PLL_SUB_SCALE, sub_tile);
     LAUNCH_CHECK();

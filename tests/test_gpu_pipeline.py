@@ -446,9 +446,9 @@ def own_queue_stream(pkg, torch_cuda):
     L.sdr_stream_destroy.argtypes = [C.c_void_p]
     made = []
 
-    def make():
+    def make(n_cu: int = 64):
         h = C.c_void_p()
-        assert L.sdr_stream_create_cu_range(C.byref(h), torch_cuda.cuda.current_device(), 0, 64, 0) == 0
+        assert L.sdr_stream_create_cu_range(C.byref(h), torch_cuda.cuda.current_device(), 0, n_cu, 0) == 0
         made.append(h.value)
         return torch_cuda.cuda.ExternalStream(h.value)
 
@@ -611,6 +611,34 @@ def test_persistent_plls_refuses_unresident_waves(pkg, torch_cuda, own_queue_str
     with pytest.raises(pkg.SdrError, match="do not fit"):
         pipe.plls_launch(2, stream=own_queue_stream())
     torch.cuda.synchronize()   # returns at once: nothing is pending
+    pipe.close()
+
+
+def test_persistent_plls_refuses_unbalanced_cu_mask(pkg, torch_cuda, own_queue_stream):
+    """1536 channels = 96 PLL waves on a 48-CU stream: 2 per CU fit the CU count, but the mask puts
+    2, 2, 1 and 1 of each XCC's 6 CUs on its four shader engines while workgroups are dealt to the
+    engines evenly, so only 64 workgroups are resident at once (tools/microbench/cumask_probe.hip,
+    profiles/r06/cumask/) -- round 5's bench hung on exactly this launch until the 5 s waits expired.
+    The launch is refused before anything is enqueued, and sdr_plls_fits says so; the SE-balanced
+    masks the bench uses are still accepted (/root/reference/include/threadsafequeue.h:24-44: the
+    producer never waits on a consumer that cannot run)."""
+    import time
+    torch = torch_cuda
+    pipe = pkg.Pipeline(1536)
+    f48 = pipe.plls_fits(48)
+    assert f48 == {"waves": 96, "groups": 96, "resident": 64, "fits": False}
+    t0 = time.perf_counter()
+    with pytest.raises(pkg.SdrError, match="do not fit"):
+        pipe.plls_launch(2, stream=own_queue_stream(48))
+    torch.cuda.synchronize()   # nothing is pending: no 5 s wait
+    assert time.perf_counter() - t0 < 2.0
+    assert pipe.plls_fits(64)["fits"]
+    pipe.close()
+    # the headline's 1024 channels: one or two waves per CU on 32 or 64 CUs, packed groups of four on
+    # 16 and 24 (the staged loop, tests/test_gpu_width.py runs 16 against the oracle)
+    pipe = pkg.Pipeline(1024)
+    for n_cu in (16, 24, 32, 64):
+        assert pipe.plls_fits(n_cu)["fits"], n_cu
     pipe.close()
 
 

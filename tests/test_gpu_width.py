@@ -39,7 +39,10 @@ def _kinds(synth):
 
 
 KEYS = ("fm", "mono", "lr", "clean", "offset", "nsym", "symbols", "nbits", "bits")
-SCHEDULES = ("dispatch", "persistent", "persistent_parts", "persistent_release")
+# persistent_packed: the PLL stream on 16 CUs -- 64 waves, four per CU in workgroups of four sharing a
+# trigArg table, the LDS-staged lane-pair loop (sdr_pll.hip pll_run_split_coal, k_pll_multi<..., 4,
+# true>) that the 2048- and 4096-channel capacity lines run
+SCHEDULES = ("dispatch", "persistent", "persistent_parts", "persistent_release", "persistent_packed")
 
 
 def _check(args):
@@ -88,8 +91,11 @@ def _run_schedule(torch, pkg, bench, iq, dev, schedule: str) -> dict:
     pipe = pkg.Pipeline(NCH, mode=0, rds_on=True, device=0)
     info = pipe.info
     created: list[int] = []
+    pll_cus = "16" if schedule == "persistent_packed" else "64"
+    if schedule == "persistent_packed":   # four waves per CU in groups of four: the staged loop
+        assert pipe.plls_fits(16) == {"waves": 64, "groups": 16, "resident": 16, "fits": True}
     try:
-        s_fe, s_pll, s_post, _ = bench.cu_masked_streams(torch, pkg, dev, "64", created)
+        s_fe, s_pll, s_post, _ = bench.cu_masked_streams(torch, pkg, dev, pll_cus, created)
     except (RuntimeError, AttributeError):
         if schedule.startswith("persistent"):
             pytest.skip("no CU-masked streams: the bench does not run the persistent PLL without them")
