@@ -20,8 +20,9 @@ HDRS     := include/sdr_amd.h $(PKG)/csrc/pll_math.h $(PKG)/csrc/sdr_internal.h
 HOSTFLAGS := -O2 -std=c++17 -fPIC -Wall -Wextra -pthread -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include \
              -Iinclude -Iinclude/dropin -I$(PKG)/host
 HOSTLIB   := $(PKG)/libsdr_host.so
-HOSTSRCS  := $(PKG)/host/dropin_primitives.cpp $(PKG)/host/dropin_stages.cpp $(PKG)/host/rds_frame.cpp
-HOSTHDRS  := $(wildcard include/dropin/*.h) $(PKG)/host/hip_util.h include/sdr_amd.h
+HOSTSRCS  := $(PKG)/host/dropin_primitives.cpp $(PKG)/host/dropin_stages.cpp $(PKG)/host/rds_frame.cpp \
+             $(PKG)/host/sdr_multi_engine.cpp
+HOSTHDRS  := $(wildcard include/dropin/*.h) $(PKG)/host/hip_util.h include/sdr_amd.h include/sdr_multi.h
 CLI       := $(PKG)/bin/sdr_project
 MULTI     := $(PKG)/bin/sdr_multi
 
@@ -54,7 +55,7 @@ $(CLI): $(PKG)/host/sdr_project.cpp $(HOSTLIB)
 	@mkdir -p $(dir $@)
 	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -lsdr_host -Wl,-rpath,'$$ORIGIN/..'
 
-$(MULTI): $(PKG)/host/sdr_multi.cpp include/dropin/fm_batch.h $(HOSTLIB)
+$(MULTI): $(PKG)/host/sdr_multi.cpp include/sdr_multi.h $(HOSTLIB)
 	@mkdir -p $(dir $@)
 	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -lsdr_host -lsdr_amd -L$(ROCM)/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/..' -Wl,-rpath,$(ROCM)/lib

@@ -923,6 +923,12 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
                 res["roofline"]["frac_of_copy"] = round(res["roofline"]["achieved"] / iso["hbm_copy"]["achieved"], 4)
                 res["roofline_fast"] = iso.get("fast")
             res["cpu_baseline"] = (None if args.no_cpu_baseline else cpu_baseline_leg(args, None, timing=(world == 1 and getattr(args, "cpu_timing", True))))
+            # the queue-plumbed program on the same input (N = 1, outside the timed region)
+            if (world == 1 and not args.no_cpu_baseline and hasattr(st, "captured") and
+                    os.environ.get("SDR_BENCH_QUEUE", "1") != "0"):
+                res["queue_plumbed"] = qp = queue_plumbed_leg(args, st, nch)
+                if "value" in qp:
+                    qp["vs_value"] = round(qp["value"] / res["value"], 4)
             if ver is not None:
                 res["cpu_baseline"]["verified"] = ver
             if gathered_check is not None:
@@ -1161,6 +1167,116 @@ def cpu_baseline_leg(args, cap: dict | None, timing: bool = True) -> dict:
     return res
 
 
+# ------------------------------------------------------------------ the queue-plumbed program
+def _multi_structs():
+    """ctypes mirrors of include/sdr_multi.h (sdr_multi_opts, sdr_multi_stats)."""
+    import ctypes as C
+
+    class Opts(C.Structure):
+        _fields_ = [("nch", C.c_int), ("mode", C.c_int), ("flags", C.c_int), ("device", C.c_int),
+                    ("pll_cus", C.c_int), ("in_path", C.c_char_p), ("d_iq", C.c_void_p),
+                    ("row_stride", C.c_size_t), ("block_stride", C.c_size_t), ("nblocks", C.c_int),
+                    ("out_prefix", C.c_char_p), ("ncap", C.c_int), ("cap_blocks", C.c_int),
+                    ("cap_ch", C.POINTER(C.c_int)), ("cap_lr", C.c_void_p), ("cap_nbits", C.c_void_p),
+                    ("cap_bits", C.c_void_p)]
+
+    class Stats(C.Structure):
+        _fields_ = [("blocks", C.c_longlong), ("seconds", C.c_double), ("steady_seconds", C.c_double),
+                    ("pll_period_ms", C.c_double), ("read_s", C.c_double), ("h2d_ms", C.c_double),
+                    ("d2h_ms", C.c_double), ("persistent", C.c_int)]
+    return Opts, Stats
+
+
+def queue_child(a) -> None:
+    """bench.py --queue-child: the multi-channel receiver engine (include/sdr_multi.h: the reference's
+    three stage threads joined by ThreadSafeQueue<FmBatch*>, threadsafequeue.h:24-74) over the bench's
+    own device-generated input (the same generator, seed and channels), in a process of its own so a
+    failure of the engine cannot take the bench line with it. Writes the captured rows of the checked
+    channels to --cap-out and prints one JSON line of the engine's timings."""
+    import ctypes as C
+    import torch
+    pkg = _load_pkg()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    iq = make_input(torch, a.channels, a.blocks, first_channel=0, device=dev)
+    host = C.CDLL(str(ROOT / "real-time-sdr_amd" / "libsdr_host.so"))
+    Opts, Stats = _multi_structs()
+    host.sdr_multi_run.argtypes = [C.POINTER(Opts), C.POINTER(Stats)]
+    host.sdr_multi_run.restype = C.c_int
+    info = pkg.Pipeline(1).info
+    ch = [int(c) for c in a.cap_ch.split(",")]
+    nb, nv = a.blocks, len(ch)
+    lr = np.zeros((nb, nv, 2 * info.n_audio), np.int16)
+    nbits = np.zeros((nb, nv), np.int32)
+    bits = np.zeros((nb, nv, pkg.SDR_MAX_BITS), np.uint8)
+    cap_ch = (C.c_int * nv)(*ch)
+    o = Opts(nch=a.channels, mode=0, flags=0, device=0, pll_cus=a.cus, in_path=None, d_iq=iq.data_ptr(),
+             row_stride=iq.stride(1), block_stride=iq.stride(0), nblocks=nb, out_prefix=None, ncap=nv,
+             cap_blocks=nb, cap_ch=cap_ch, cap_lr=lr.ctypes.data, cap_nbits=nbits.ctypes.data,
+             cap_bits=bits.ctypes.data)
+    st = Stats()
+    torch.cuda.synchronize(dev)
+    rc = host.sdr_multi_run(C.byref(o), C.byref(st))
+    if rc != 0:
+        raise SystemExit(f"sdr_multi_run: {rc} {pkg.lib().sdr_last_error()}")
+    np.savez(a.cap_out, lr=lr, nbits=nbits, bits=bits)
+    import hashlib
+    iq_sha = hashlib.sha256(np.ascontiguousarray(iq[:, ch].cpu().numpy()).tobytes()).hexdigest()
+    print(json.dumps({"iq_sha": iq_sha, "blocks": st.blocks, "seconds": st.seconds, "steady_seconds": st.steady_seconds,
+                      "pll_period_ms": st.pll_period_ms, "d2h_ms": st.d2h_ms, "persistent": st.persistent,
+                      "block_iq": info.block_iq}), flush=True)
+
+
+def queue_plumbed_leg(args, st, nch: int) -> dict:
+    """Rank 0 at N = 1, outside the timed region: the same channels and blocks through the
+    queue-plumbed receiver (queue_child), its rate next to `value`, and its captured stereo audio and
+    RDS bits compared with the bench's own captures of the same channels (which the checker compared
+    with the oracle): equal rows mean the queue program is verified against the oracle too."""
+    import tempfile
+    cap = st.captured()
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "cap.npz")
+        cus = int(st.cu_spec) if str(getattr(st, "cu_spec", "")).isdigit() else 64
+        cmd = [sys.executable, str(pathlib.Path(__file__).resolve()), "--queue-child", "--channels", str(nch),
+               "--blocks", str(st.nblocks), "--cus", str(cus), "--cap-ch", ",".join(str(c) for c in cap["channels"]),
+               "--cap-out", out]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        except subprocess.SubprocessError as exc:
+            return {"error": str(exc)}
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"error": f"exit {r.returncode}: {r.stderr[-500:]}"}
+        q = json.loads(lines[-1])
+        import hashlib
+        if q["iq_sha"] != hashlib.sha256(np.ascontiguousarray(cap["iq"]).tobytes()).hexdigest():
+            return {"error": "the child's regenerated input differs from the bench's"}
+        got = np.load(out)
+        equal = np.array_equal(got["lr"], cap["lr"]) and np.array_equal(got["nbits"], cap["nbits"])
+        for b, j in np.argwhere(cap["nbits"] > 0) if equal else ():   # the bits a row holds
+            k = int(cap["nbits"][b, j])
+            equal = equal and np.array_equal(got["bits"][b, j, :k], cap["bits"][b, j, :k])
+    samples = nch * q["block_iq"]
+    res = {
+        "program": "real-time-sdr_amd/host/sdr_multi_engine.cpp (include/sdr_multi.h): RF / audio / RDS threads "
+                   "(project.cpp:134-136), ThreadSafeQueue<FmBatch*> (threadsafequeue.h:24-74) with device-resident "
+                   "fm_demod batches, one context per thread, each consumer's PLL as its own persistent launch "
+                   "(sdr_plls_launch_sel), L/R PCM and RDS bits copied to the host every block",
+        "input": f"the bench's device-generated input, same channels and blocks ({q['blocks']} blocks incl. the "
+                 f"warm-up), regenerated in a child process",
+        "value": round(q["blocks"] * samples / q["seconds"] / 1e6, 2), "unit": "MS/s",
+        "ms_per_block": round(q["seconds"] / q["blocks"] * 1e3, 4),
+        "steady_value": (round((q["blocks"] - 1) * samples / q["steady_seconds"] / 1e6, 2)
+                         if q["steady_seconds"] else None),
+        "pll_period_ms": round(q["pll_period_ms"], 4),
+        "pll": "persistent" if q["persistent"] else "per-block dispatch",
+        "d2h_ms": round(q["d2h_ms"], 2),
+        "outputs_equal_to_bench_capture": bool(equal),
+        "checked_channels": cap["channels"],
+    }
+    return res
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1177,8 +1293,16 @@ def main() -> None:
     ap.add_argument("--numerics", choices=("exact", "fast"), default="exact",
                     help="exact: every output bit-identical to the reference; fast: the matrix-core front end "
                          "(fm_demod within 1e-5, RDS bits bit-exact)")
+    ap.add_argument("--queue-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--blocks", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--cus", type=int, default=64, help=argparse.SUPPRESS)
+    ap.add_argument("--cap-ch", default="0", help=argparse.SUPPRESS)
+    ap.add_argument("--cap-out", default="", help=argparse.SUPPRESS)
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
+    if args.queue_child:
+        queue_child(args)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -213,10 +213,20 @@ int sdr_plls(sdr_ctx *ctx, void *stream);
  * again while blocks of the previous launch were never signalled first lets that launch time out
  * and drain. Not with SDR_FLAG_PLL_LIBM. */
 int sdr_plls_launch(sdr_ctx *ctx, int nblocks, void *stream);
-/* Would sdr_plls_launch accept a stream made by sdr_stream_create_cu_range(first_cu, n_cu, exclude
- * = 0) for this context? Fills the launch's waves, its workgroups and how many of them that CU range
- * keeps resident at once; it fits when *groups <= *resident. No stream is made, nothing is enqueued. */
-int sdr_plls_fits(sdr_ctx *ctx, int first_cu, int n_cu, int *waves, long long *groups, long long *resident);
+/* The same for one of the two PLLs (which = SDR_PLLS_STEREO or SDR_PLLS_RDS; SDR_PLLS_BOTH is
+ * sdr_plls_launch): for a context that runs one chain only, as each consumer thread of the reference
+ * does (project.cpp:134-136: stereo in the audio thread, RDS in the rds thread). sdr_plls_signal
+ * then needs only that chain's _pre part, and only that chain's _post part follows the wait. */
+#define SDR_PLLS_STEREO 1
+#define SDR_PLLS_RDS 2
+#define SDR_PLLS_BOTH 3
+int sdr_plls_launch_sel(sdr_ctx *ctx, int nblocks, int which, void *stream);
+/* Would sdr_plls_launch_sel(which) accept a stream made by sdr_stream_create_cu_range(first_cu, n_cu,
+ * exclude = 0) for this context? Fills the launch's waves, its workgroups and how many of them that
+ * CU range keeps resident at once; it fits when *groups <= *resident. No stream is made, nothing is
+ * enqueued. */
+int sdr_plls_fits(sdr_ctx *ctx, int which, int first_cu, int n_cu, int *waves, long long *groups,
+                  long long *resident);
 /* Optional, ahead of sdr_plls_launch(nblocks) (e.g. before a timed region): the launch's
  * bookkeeping -- allocation, the reset of its stamps and error word -- in `stream`'s order, so the
  * launch itself only enqueues the kernel. Ignored by a launch with another nblocks. */

@@ -100,7 +100,8 @@ def lib() -> C.CDLL:
         "sdr_plls": ([vp, vp], i32),
         "sdr_plls_launch": ([vp, i32, vp], i32),
         "sdr_plls_prepare": ([vp, i32, vp], i32),
-        "sdr_plls_fits": ([vp, i32, i32, C.POINTER(i32), C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)], i32),
+        "sdr_plls_fits": ([vp, i32, i32, i32, C.POINTER(i32), C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)], i32),
+        "sdr_plls_launch_sel": ([vp, i32, i32, vp], i32),
         "sdr_plls_signal": ([vp, vp], i32),
         "sdr_frontend_pre_parts": ([vp, vp, sz, i32, vp], i32),
         "sdr_plls_wait": ([vp, vp], i32),
@@ -359,14 +360,17 @@ class Pipeline:
         check(lib().sdr_plls(self._h, _stream(stream)), "sdr_plls")
 
     # persistent PLLs (include/sdr_amd.h): one dispatch for many blocks
-    def plls_launch(self, nblocks: int, stream=None):
-        check(lib().sdr_plls_launch(self._h, nblocks, _stream(stream)), "sdr_plls_launch")
+    def plls_launch(self, nblocks: int, stream=None, which: int = 3):
+        """Persistent PLLs of the next nblocks blocks (which = 3: both; 1: stereo, 2: RDS only)."""
+        check(lib().sdr_plls_launch_sel(self._h, nblocks, which, _stream(stream)), "sdr_plls_launch_sel")
 
-    def plls_fits(self, n_cu: int, first_cu: int = 0) -> dict:
-        """Would plls_launch accept a stream over CUs [first_cu, first_cu + n_cu)? The launch's waves,
-        workgroups and how many of those the range keeps resident at once (sdr_plls_fits)."""
+    def plls_fits(self, n_cu: int, first_cu: int = 0, which: int = 3) -> dict:
+        """Would plls_launch (which = 3: both PLLs; 1 stereo, 2 RDS: plls_launch_sel) accept a stream
+        over CUs [first_cu, first_cu + n_cu)? The launch's waves, workgroups and how many of those the
+        range keeps resident at once (sdr_plls_fits)."""
         w, g, r = C.c_int(), C.c_longlong(), C.c_longlong()
-        check(lib().sdr_plls_fits(self._h, first_cu, n_cu, C.byref(w), C.byref(g), C.byref(r)), "sdr_plls_fits")
+        check(lib().sdr_plls_fits(self._h, which, first_cu, n_cu, C.byref(w), C.byref(g), C.byref(r)),
+              "sdr_plls_fits")
         return {"waves": w.value, "groups": g.value, "resident": r.value, "fits": g.value <= r.value}
 
     def plls_prepare(self, nblocks: int, stream=None):

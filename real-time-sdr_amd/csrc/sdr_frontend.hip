@@ -12,6 +12,14 @@
 
 #pragma clang fp contract(off)
 
+// Diagnosis builds only (timing, wrong outputs; tools/build_variant.sh FEFLAGS=-DSDR_FE_DIAG=n):
+// bit 0 -- k_frontend2 multiplies the raw window words instead of converted samples (no
+// conversion), bit 1 -- no discriminator division, bit 2 -- every workgroup stages the same
+// L2-resident window. The product build is SDR_FE_DIAG = 0.
+#ifndef SDR_FE_DIAG
+#define SDR_FE_DIAG 0
+#endif
+
 namespace sdrk {
 namespace {
 // ------------------------------------------------------------------------------------------
@@ -364,6 +372,15 @@ __global__ __launch_bounds__(64) void k_frontend2(
     const int c0 = j * ADV - 1;                       // first decimated output (the carry)
     const int m0 = c0 * D - HP;                       // first staged sample
     const uint8_t* src = iq + (size_t)ch * iq_stride;
+#if SDR_FE_DIAG & 4
+    // diagnosis: every workgroup stages channel 0's second tile (L2-resident input, staging latency
+    // without HBM misses)
+    const int m0s = ADV * D - D - HP;
+    const uint8_t* srcs = iq;
+#else
+    const int m0s = m0;
+    const uint8_t* srcs = src;
+#endif
     {
         // window -> LDS (lane t holds dwords t, t+64, ...). Every I/Q sample is one u16; samples
         // before the block come from the previous block's tail, samples past its end are u8 128.
@@ -372,8 +389,8 @@ __global__ __launch_bounds__(64) void k_frontend2(
         uint32_t* sd = reinterpret_cast<uint32_t*>(sw);
         const uint8_t* tin = tail_in + (size_t)ch * 2 * HP;
         if (D % 2 == 0) {
-            if (m0 >= 0 && m0 + WIN <= block_iq) {
-                const uint32_t* g = reinterpret_cast<const uint32_t*>(src + 2 * m0);
+            if (m0s >= 0 && m0s + WIN <= block_iq) {
+                const uint32_t* g = reinterpret_cast<const uint32_t*>(srcs + 2 * m0s);
                 uint32_t pf[PER];
 #pragma unroll
                 for (int k = 0; k < PER; k++) {
@@ -383,7 +400,7 @@ __global__ __launch_bounds__(64) void k_frontend2(
 #pragma unroll
                 for (int k = 0; k < PER; k++) {
                     const int i = t + NTH * k;
-                    if (k < PER - 1 || i < NG) sd[i] = pf[k];
+                    if (k < PER - 1 || i < NG) sd[i] = pf[k] ^ 0x80808080u;
                 }
             } else {
                 const uint32_t* gs = reinterpret_cast<const uint32_t*>(src);
@@ -392,7 +409,7 @@ __global__ __launch_bounds__(64) void k_frontend2(
                     const int mm = m0 + 2 * i;
                     const uint32_t* pa = mm >= 0 ? (mm < block_iq ? gs + (mm >> 1) : pad)
                                                  : (mm >= -HP ? gt + ((HP + mm) >> 1) : pad);
-                    sd[i] = *pa;
+                    sd[i] = *pa ^ 0x80808080u;
                 }
             }
         } else {
@@ -407,7 +424,7 @@ __global__ __launch_bounds__(64) void k_frontend2(
                     if (m < -HP || m >= block_iq) pa = reinterpret_cast<const uint16_t*>(pad);
                     v |= (uint32_t)*pa << (16 * h);
                 }
-                sd[i] = v;
+                sd[i] = v ^ 0x80808080u;
             }
         }
     }
@@ -441,8 +458,12 @@ __global__ __launch_bounds__(64) void k_frontend2(
     auto sample = [&](int S) -> f32x2 {
         const uint4 c4 = chunk[S >> 3];
         const int dw = (S & 7) >> 1;
-        const uint32_t w = (dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w) ^ 0x80808080u;
+        const uint32_t w = dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w;   // signed bytes (staging)
+#if SDR_FE_DIAG & 1
+        return f32x2{__builtin_bit_cast(float, w & 0x3F3F3F3Fu), __builtin_bit_cast(float, w & 0x3E3E3E3Eu)};
+#else
         return (S & 1) ? fe_cvt_v<1>(w) : fe_cvt_v<0>(w);
+#endif
     };
     // one sample of look-ahead: sample S-1 is converted while sample S's MACs issue
     f32x2 m_next = sample(TWIN - 1);
@@ -485,6 +506,9 @@ __global__ __launch_bounds__(64) void k_frontend2(
         }
         const f32x2 cur = acc[r];
         float v;
+#if SDR_FE_DIAG & 2
+        v = cur.x + pv.y;
+#else
         if ((cur.x == 0) & (cur.y == 0)) {
             v = 0.0f;
         } else {
@@ -492,6 +516,7 @@ __global__ __launch_bounds__(64) void k_frontend2(
             const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
             v = (float)((double)num / den);
         }
+#endif
         if (c > c0 && c >= 0 && c < block_if) out[c] = v;
         if (c == block_if - 1) prev_out[ch] = make_float2(cur.x, cur.y);
     }

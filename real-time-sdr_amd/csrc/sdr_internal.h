@@ -141,8 +141,9 @@ struct CuPlacement {
     long long resident(int per_cu) const { return (long long)xcc_active * min_units * per_cu; }
 };
 CuPlacement cu_placement(const uint32_t* mask, int nwords, int ncu_dev, int nxcc);
-// the persistent PLL launch's shape for these jobs: kernel, workgroups, waves, and how many of its
-// workgroups the placement keeps resident at once (resident < groups: the launch would hang)
+// the persistent PLL launch's shape for jobs.p[k].j[0 .. njobs) (njobs = 2: the stereo and RDS PLLs,
+// 1: one of them): kernel, workgroups, waves, and how many of its workgroups the placement keeps
+// resident at once (resident < groups: the launch would hang)
 struct PllMultiPlan {
     const void* kern = nullptr;
     int WG = 1, tab_ok = 0, per_cu = 0;
@@ -151,8 +152,8 @@ struct PllMultiPlan {
     uint32_t waves = 0;
     long long groups = 0, resident = 0;
 };
-int pll_multi_plan(const PllJobs2& jobs, int n, int nch, const CuPlacement& pl, PllMultiPlan* plan);
-int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
+int pll_multi_plan(const PllJobs2& jobs, int njobs, int n, int nch, const CuPlacement& pl, PllMultiPlan* plan);
+int launch_pll_multi(const PllJobs2& jobs, int njobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
                      hipStream_t s, const CuPlacement& pl,   // refused unless every workgroup is resident at once
                      int sub_tile);                 // > 0: the first block's input may come in parts of this many samples
@@ -223,6 +224,7 @@ struct sdr_ctx {
     int pers_prepared = 0;                              // sdr_plls_prepare's nblocks (0: none pending)
     uint32_t pers_prepared_launch = 0;                  // pers_launched when it was prepared
     uint32_t pers_launched = 0, pers_signaled = 0, pers_waves = 0;
+    int pers_which = SDR_PLLS_BOTH;                     // the PLLs the last launch runs (sdr_plls_launch_sel)
     uint32_t pers_base = 0;                             // sequence number of the last launch's first block
     uint32_t pers_waited = 0;                           // sequence numbers below this have been waited for
     long long pers_first_block = -1;                    // the context block that sequence number belongs to

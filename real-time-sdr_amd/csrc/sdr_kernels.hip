@@ -2542,23 +2542,33 @@ int sdr_plls_prepare(sdr_ctx* c, int nblocks, void* stream) {
     return plls_prepare(c, nblocks, S(stream));
 }
 
-// the persistent launch's jobs: both PLLs of the two parities, p[0] = the parity the next
-// sdr_frontend switches to
-static PllJobs2 plls_jobs(sdr_ctx* c) {
+// the persistent launch's jobs: the selected PLLs (SDR_PLLS_STEREO, SDR_PLLS_RDS; in that order in
+// j[]) of the two parities, p[0] = the parity the next sdr_frontend switches to
+static PllJobs2 plls_jobs(sdr_ctx* c, int which, int* njobs) {
     PllJobs2 jobs{};
     const int first_parity = c->parity ^ 1;
     for (int k = 0; k < 2; k++) {
         const int saved = c->parity;
         c->parity = first_parity ^ k;
-        jobs.p[k].j[0] = stereo_job(c);
-        jobs.p[k].j[1] = rds_job(c);
+        int q = 0;
+        if (which & SDR_PLLS_STEREO) jobs.p[k].j[q++] = stereo_job(c);
+        if (which & SDR_PLLS_RDS) jobs.p[k].j[q++] = rds_job(c);
+        *njobs = q;
         c->parity = saved;
     }
     return jobs;
 }
 
-int sdr_plls_fits(sdr_ctx* c, int first_cu, int n_cu, int* waves, long long* groups, long long* resident) {
+static int plls_which_ok(const sdr_ctx* c, int which, const char* what) {
+    if (which != SDR_PLLS_STEREO && which != SDR_PLLS_RDS && which != SDR_PLLS_BOTH)
+        return fail(SDR_E_INVALID, "%s: which = %d (SDR_PLLS_STEREO, SDR_PLLS_RDS or SDR_PLLS_BOTH)", what, which);
+    if ((which & SDR_PLLS_RDS) && !c->rds_on) return fail(SDR_E_INVALID, "%s: the RDS PLL needs rds_on", what);
+    return SDR_OK;
+}
+
+int sdr_plls_fits(sdr_ctx* c, int which, int first_cu, int n_cu, int* waves, long long* groups, long long* resident) {
     if (!c || !waves || !groups || !resident) return fail(SDR_E_INVALID, "plls_fits: bad arguments");
+    if (const int r = plls_which_ok(c, which, "plls_fits")) return r;
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, c->device));
     const int ncu = prop.multiProcessorCount;
@@ -2568,18 +2578,23 @@ int sdr_plls_fits(sdr_ctx* c, int first_cu, int n_cu, int* waves, long long* gro
     const std::vector<uint32_t> mask = cu_range_mask(ncu, first_cu, n_cu, 0, &nset);
     const CuPlacement pl = cu_placement(mask.data(), (int)mask.size(), ncu, device_xccs(c->device));
     HIP_TRY(hipSetDevice(c->device));
+    int njobs = 0;
+    const PllJobs2 jobs = plls_jobs(c, which, &njobs);
     PllMultiPlan P;
-    if (const int r = pll_multi_plan(plls_jobs(c), c->info.block_if, c->nch, pl, &P)) return r;
+    if (const int r = pll_multi_plan(jobs, njobs, c->info.block_if, c->nch, pl, &P)) return r;
     *waves = (int)P.waves;
     *groups = P.groups;
     *resident = P.resident;
     return SDR_OK;
 }
 
-int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
+int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) { return sdr_plls_launch_sel(c, nblocks, SDR_PLLS_BOTH, stream); }
+
+int sdr_plls_launch_sel(sdr_ctx* c, int nblocks, int which, void* stream) {
     if (!c || nblocks <= 0) return fail(SDR_E_INVALID, "plls_launch: bad arguments");
     if (const int rf_ = check_failed(c, "plls_launch")) return rf_;
     if (c->flags & SDR_FLAG_PLL_LIBM) return fail(SDR_E_INVALID, "plls_launch: not with SDR_FLAG_PLL_LIBM");
+    if (const int r = plls_which_ok(c, which, "plls_launch")) return r;
     hipStream_t s = S(stream);
     // the launch's waves spin until later dispatches on other streams publish each block, so the
     // PLL stream must own its hardware queue (pool streams share GPU_MAX_HW_QUEUES queues with the
@@ -2595,10 +2610,11 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
         return fail(SDR_E_INVALID, "plls_launch: the PLL stream is on device %d, the context on %d", sdev, c->device);
     HIP_TRY(hipSetDevice(c->device));
     const int n = c->info.block_if, nch = c->nch;
-    const PllJobs2 jobs = plls_jobs(c);
+    int njobs = 0;
+    const PllJobs2 jobs = plls_jobs(c, which, &njobs);
     {
         PllMultiPlan P;
-        if (const int r = pll_multi_plan(jobs, n, nch, pl, &P)) return r;
+        if (const int r = pll_multi_plan(jobs, njobs, n, nch, pl, &P)) return r;
         if (P.groups > P.resident)
             return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit the stream's %d CUs: %lld of %lld workgroups "
                         "of %d waves resident at once (%d per CU, %d XCCs x %d SE-balanced CU slots; use sdr_plls, "
@@ -2613,9 +2629,10 @@ int sdr_plls_launch(sdr_ctx* c, int nblocks, void* stream) {
     }
     c->pers_prepared = 0;
     uint32_t waves = 0;
-    const int r = launch_pll_multi(jobs, n, nch, nblocks, c->pers_words, c->pers_launched, c->pers_t0, c->pers_t1,
-                                   c->pers_cyc, &waves, s, pl, FRB_TILE);
+    const int r = launch_pll_multi(jobs, njobs, n, nch, nblocks, c->pers_words, c->pers_launched, c->pers_t0,
+                                   c->pers_t1, c->pers_cyc, &waves, s, pl, FRB_TILE);
     if (r) return r;
+    c->pers_which = which;
     c->pers_failed = false;   // this launch's error word was cleared by its prepare
     c->pers_waves = waves;
     c->pers_base = c->pers_launched;
@@ -2655,6 +2672,8 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
         return fail(SDR_E_INVALID, "frontend_pre_parts: needs rds_on, 101 taps and the exact front end");
     if (c->pers_signaled != c->pers_base)
         return fail(SDR_E_INVALID, "frontend_pre_parts: only the first block of a persistent launch comes in parts");
+    if (c->pers_which != SDR_PLLS_BOTH)
+        return fail(SDR_E_INVALID, "frontend_pre_parts: the launch must cover both PLLs (sdr_plls_launch)");
     if (const int r = plls_signal_check(c, c->block + 1, "frontend_pre_parts")) return r;
     hipStream_t s = S(stream);
     const int n = c->info.block_if, ntiles = cdiv(n, FRB_TILE), fe_tiles = frontend_tiles(n);
@@ -2693,16 +2712,19 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
 int sdr_plls_signal(sdr_ctx* c, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (const int rf_ = check_failed(c, "plls_signal")) return rf_;
-    if (c->st_pre_done != c->block || c->rds_pre_done != c->block || c->st_pll_done == c->block ||
-        c->rds_pll_done == c->block)
-        return fail(SDR_E_INVALID, "plls_signal: run sdr_stereo_pre and sdr_rds_pre on a new block first");
+    const bool st = (c->pers_which & SDR_PLLS_STEREO) != 0, rd = (c->pers_which & SDR_PLLS_RDS) != 0;
+    if ((st && (c->st_pre_done != c->block || c->st_pll_done == c->block)) ||
+        (rd && (c->rds_pre_done != c->block || c->rds_pll_done == c->block)))
+        return fail(SDR_E_INVALID, "plls_signal: run the pre part of every PLL the launch covers (sdr_stereo_pre, "
+                                   "sdr_rds_pre) on a new block first");
     if (const int rc = plls_signal_check(c, c->block, "plls_signal")) return rc;
     const int r = launch_flag_store(c->pers_words, c->pers_signaled + 1u, S(stream));
     if (r) return r;
     c->pers_block = c->block;
     c->pers_block_seq = c->pers_signaled;
     c->pers_signaled++;
-    c->st_pll_done = c->rds_pll_done = c->block;
+    if (st) c->st_pll_done = c->block;
+    if (rd) c->rds_pll_done = c->block;
     return SDR_OK;
 }
 

@@ -1303,10 +1303,10 @@ int launch_pll(bool libm, const float* in, size_t in_stride, int n, int nch, flo
     return launch_plls(libm, jobs, 1, n, nch, s);
 }
 
-int pll_multi_plan(const PllJobs2& jobs, int n, int nch, const CuPlacement& pl, PllMultiPlan* plan) {
+int pll_multi_plan(const PllJobs2& jobs, int njobs, int n, int nch, const CuPlacement& pl, PllMultiPlan* plan) {
     bool vec = true, split = true;
     for (int k = 0; k < 2; k++)
-        for (int q = 0; q < 2; q++) {
+        for (int q = 0; q < njobs; q++) {
             const PllJob& j = jobs.p[k].j[q];
             vec = vec && (reinterpret_cast<uintptr_t>(j.in) % 16 == 0) && (j.in_stride % 4 == 0) &&
                   (reinterpret_cast<uintptr_t>(j.tbuf) % 16 == 0) && (j.t_stride % 4 == 0) &&
@@ -1318,11 +1318,11 @@ int pll_multi_plan(const PllJobs2& jobs, int n, int nch, const CuPlacement& pl, 
     const size_t tab_bytes = round_up((size_t)std::max(n, 1), 2) * sizeof(double);
     P.tab_ok = tab_bytes <= 64 * 1024 ? 1 : 0;
     P.lds = P.tab_ok ? tab_bytes : 0;
-    const int wave_cnt = cdiv(split ? 2 * nch : nch, 64) * 2;
+    const int wave_cnt = cdiv(split ? 2 * nch : nch, 64) * njobs;
     // one wave per workgroup (its own CU time slice and table) while two tables per CU fit the
     // stream's CUs, else groups of 4 waves -- one per SIMD -- sharing one table per CU
     P.WG = wave_cnt > 2 * pl.ncu ? 4 : 1;
-    P.g = dim3(cdiv(split ? 2 * nch : nch, 64 * P.WG), 2);
+    P.g = dim3(cdiv(split ? 2 * nch : nch, 64 * P.WG), njobs);
     P.b = dim3(64 * P.WG);
     P.waves = P.g.x * P.g.y * P.WG;
     P.groups = (long long)P.g.x * P.g.y;
@@ -1369,11 +1369,11 @@ int pll_multi_plan(const PllJobs2& jobs, int n, int nch, const CuPlacement& pl, 
     return SDR_OK;
 }
 
-int launch_pll_multi(const PllJobs2& jobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
+int launch_pll_multi(const PllJobs2& jobs, int njobs, int n, int nch, int nblocks, uint32_t* words, uint32_t pre_first,
                      unsigned long long* t0, unsigned long long* t1, unsigned long long* tc, uint32_t* waves,
                      hipStream_t s, const CuPlacement& pl, int sub_tile) {
     PllMultiPlan P;
-    if (const int r = pll_multi_plan(jobs, n, nch, pl, &P)) return r;
+    if (const int r = pll_multi_plan(jobs, njobs, n, nch, pl, &P)) return r;
     *waves = P.waves;
     if (P.groups > P.resident)
         return fail(SDR_E_INVALID, "plls_launch: %u waves do not fit the stream's %d CUs: %lld of %lld workgroups of "

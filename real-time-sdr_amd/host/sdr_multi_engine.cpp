@@ -1,0 +1,575 @@
+// sdr_multi_engine.cpp -- the multi-channel receiver engine (include/sdr_multi.h): the reference
+// program's three stage threads (project.cpp:134-136: RF front end, audio, RDS) over nch channels at
+// once, on the C ABI of libsdr_amd.so, joined by the reference's queue protocol with the payload on
+// the device (include/dropin/fm_batch.h). The CLI real-time-sdr_amd/bin/sdr_multi (sdr_multi.cpp) and
+// bench.py's queue_plumbed leg run it.
+//
+// Threads (per block b; every device hand-off is a HIP event or a device flag, no thread waits for
+// another's GPU work except through the queue's prepare() ordering):
+//   reader  file/stdin -> pinned ring slot (byte-stream input only)
+//   RF      [slot -H2D (copy stream)-> d_iq] or the device-resident block; sdr_frontend; fm_demod ->
+//           a recycled FmBatch (device), event, push                     rffrontend.cpp:45-76
+//   audio   wait_and_pop(0); sdr_push_fm_demod; stereo_pre; PLL; stereo_post; L/R -D2H-> pinned;
+//           the write of block b-1 overlaps the GPU work of block b          stereo.cpp:69-114
+//   rds     wait_and_pop(1); sdr_push_fm_demod; rds_pre; PLL; rds_post; rds_bits -D2H-> host;
+//           frame sync per channel every 15 decoding blocks (host)          rds.cpp:95-192
+// Streams (the four-queue budget of DESIGN.md 5): the producer's front end and both consumers' pre
+// parts share one stream (s_fe), both consumers' post parts another (s_post), and each consumer's
+// PLL has its own CU-masked stream -- with a known block count ONE persistent launch per consumer
+// (sdr_plls_launch_sel: the stereo PLL on CUs [0, pll_cus/2), the RDS PLL on [pll_cus/2, pll_cus)),
+// signalled from s_fe and waited for on s_post; otherwise one dispatch per block. s_fe and s_post
+// run on the CUs the PLLs leave. A consumer's wait on s_post is enqueued after its signal on s_fe
+// and its next parity reuse on s_fe after its post on s_post, so no wait on one stream can sit in
+// front of the work it waits for on the other.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <iostream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+
+#include <sys/stat.h>
+#include <unistd.h>
+#include <vector>
+
+#include "fm_batch.h"
+#include "hip_util.h"
+#include "rds_utilities.h"
+#include "sdr_amd.h"
+#include "sdr_multi.h"
+
+using sdrhost::check_hip;
+using sdrhost::check_sdr;
+using sdrhost::die;
+
+namespace {
+
+hipStream_t plain_stream() {
+    hipStream_t h = nullptr;
+    check_hip(hipStreamCreateWithFlags(&h, hipStreamNonBlocking), "hipStreamCreate");
+    return h;
+}
+
+// a stream on CUs [first, first + n) (exclude = 0) or on every other CU (exclude = 1); its own
+// hardware queue (sdr_stream_create_cu_range)
+hipStream_t masked_stream(int device, int first, int n, int exclude) {
+    void* s = nullptr;
+    check_sdr(sdr_stream_create_cu_range(&s, device, first, n, exclude), "sdr_stream_create_cu_range");
+    return (hipStream_t)s;
+}
+
+hipEvent_t new_event() {
+    hipEvent_t e = nullptr;
+    check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    return e;
+}
+
+// ------------------------------------------------------------------ reader: input -> pinned ring
+struct Reader {
+    static constexpr int SLOTS = 4;   // pinned input slots: the read of block b+2..b+3 rides out host jitter
+    FILE* f = nullptr;
+    size_t bytes = 0;
+    uint8_t* slot[SLOTS] = {};
+    hipEvent_t consumed[SLOTS] = {};    // the H2D copy out of the slot has completed
+    bool armed[SLOTS] = {};
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<int> filled, empty;
+    bool eof = false;
+    double read_s = 0.0;                // time spent reading (the input side of the I/O)
+    int readers = 8;                    // pread threads per block (regular files; SDR_MULTI_READERS)
+    long long file_size = 0, offset = 0;
+    std::thread th;
+
+    Reader(const std::string& path, size_t block_bytes) : bytes(block_bytes) {
+        f = path == "-" ? stdin : std::fopen(path.c_str(), "rb");
+        if (!f) die("cannot open " + path);
+        if (f != stdin) {   // a regular file is read by several threads at once (pread of a block's parts)
+            struct stat sb;
+            if (fstat(fileno(f), &sb) == 0 && S_ISREG(sb.st_mode)) {
+                file_size = (long long)sb.st_size;
+                if (const char* e = std::getenv("SDR_MULTI_READERS")) readers = std::max(1, std::atoi(e));
+            } else {
+                readers = 1;
+            }
+        } else {
+            readers = 1;
+        }
+        for (int i = 0; i < SLOTS; i++) {
+            check_hip(hipHostMalloc(reinterpret_cast<void**>(&slot[i]), bytes, hipHostMallocDefault), "hipHostMalloc");
+            consumed[i] = new_event();
+            empty.push_back(i);
+        }
+        th = std::thread([this] { run(); });
+    }
+    void run() {
+        for (;;) {
+            int i;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [this] { return !empty.empty(); });
+                i = empty.front();
+                empty.pop_front();
+            }
+            if (armed[i]) check_hip(hipEventSynchronize(consumed[i]), "hipEventSynchronize");
+            const auto r0 = std::chrono::steady_clock::now();
+            const size_t got = readers > 1 ? pread_block(slot[i]) : std::fread(slot[i], 1, bytes, f);
+            read_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - r0).count();
+            std::lock_guard<std::mutex> lk(m);
+            if (got < bytes) {             // a partial block ends the stream (rffrontend.cpp:50-52)
+                eof = true;
+                cv.notify_all();
+                return;
+            }
+            filled.push_back(i);
+            cv.notify_all();
+        }
+    }
+    // one block by `readers` threads, each a contiguous part (pread at the block's file offset)
+    size_t pread_block(uint8_t* dst) {
+        if (offset + (long long)bytes > file_size) return 0;   // a partial block ends the stream
+        const size_t part = (bytes / readers + 4095) / 4096 * 4096;
+        std::vector<std::thread> th_;
+        std::vector<size_t> got_(readers, 0);
+        for (int r = 0; r < readers; r++) {
+            const size_t lo = std::min(bytes, part * r), hi = std::min(bytes, part * (r + 1));
+            th_.emplace_back([&, r, lo, hi] {
+                size_t done = 0;
+                while (lo + done < hi) {
+                    const ssize_t k = ::pread(fileno(f), dst + lo + done, hi - lo - done, offset + (long long)(lo + done));
+                    if (k <= 0) break;
+                    done += (size_t)k;
+                }
+                got_[r] = done;
+            });
+        }
+        size_t got = 0;
+        for (int r = 0; r < readers; r++) {
+            th_[r].join();
+            got += got_[r];
+        }
+        offset += (long long)got;
+        return got;
+    }
+    int next() {   // a filled slot, or -1 at the end of the input
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [this] { return !filled.empty() || eof; });
+        if (filled.empty()) return -1;
+        const int i = filled.front();
+        filled.pop_front();
+        return i;
+    }
+    void release(int i, hipStream_t copy_stream) {   // after the H2D copy of slot i is enqueued
+        check_hip(hipEventRecord(consumed[i], copy_stream), "hipEventRecord");
+        std::lock_guard<std::mutex> lk(m);
+        armed[i] = true;
+        empty.push_back(i);
+        cv.notify_all();
+    }
+    ~Reader() {
+        if (th.joinable()) th.join();
+        for (int i = 0; i < SLOTS; i++) (void)hipHostFree(slot[i]);
+        if (f && f != stdin) std::fclose(f);
+    }
+};
+
+struct Shared {
+    sdr_multi_opts o{};
+    sdr_info info{};
+    ThreadSafeQueue<FmBatch*> q;
+    sdr_ctx* ctx[3] = {};                // RF, audio, RDS (each thread owns its context)
+    hipStream_t s_fe = nullptr, s_post = nullptr, s_pll[2] = {}, s_copy = nullptr;
+    bool persistent = false;
+    long long nblocks_known = -1;        // -1: a byte stream of unknown length
+    long long blocks = 0;
+    double read_s = 0.0, h2d_ms = 0.0, d2h_ms = 0.0;   // input reads; GPU time of the H2D / L+R D2H copies
+    std::chrono::steady_clock::time_point t_block1{};  // block 1's front end enqueued
+};
+
+hipEvent_t timing_event() {
+    hipEvent_t e = nullptr;
+    check_hip(hipEventCreate(&e), "hipEventCreate");
+    return e;
+}
+float elapsed_ms(hipEvent_t a, hipEvent_t b) {
+    check_hip(hipEventSynchronize(b), "hipEventSynchronize");
+    float ms = 0.0f;
+    check_hip(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+    return ms;
+}
+
+// ------------------------------------------------------------------ RF front end (producer)
+void rf_thread(Shared* sh) {
+    const sdr_multi_opts& o = sh->o;
+    check_hip(hipSetDevice(o.device), "hipSetDevice");
+    sdr_ctx* ctx = sh->ctx[0];
+    const sdr_info& in = sh->info;
+    const size_t row = 2 * (size_t)in.block_iq, bytes = row * o.nch;
+    hipStream_t s = sh->s_fe;
+    const bool dev_in = o.in_path == nullptr;
+    uint8_t* d_iq[2] = {};
+    hipEvent_t h2d[2] = {}, fe_done[2] = {};
+    // copy timing: a ring of event pairs, read without blocking the producer (a pair is waited for
+    // only when the ring wraps onto a copy that has not finished)
+    constexpr int TR = 8;
+    hipEvent_t c0[TR] = {}, c1[TR] = {};
+    long long timed = 0;                                    // blocks whose copy time is in h2d_ms
+    auto harvest = [&](long long upto, bool wait) {
+        for (; timed < upto; timed++) {
+            const int t = (int)(timed % TR);
+            if (!wait && hipEventQuery(c1[t]) == hipErrorNotReady) break;
+            sh->h2d_ms += elapsed_ms(c0[t], c1[t]);
+        }
+    };
+    Reader* rd = nullptr;
+    if (!dev_in) {
+        for (int k = 0; k < 2; k++) {
+            check_hip(hipMalloc(reinterpret_cast<void**>(&d_iq[k]), bytes), "hipMalloc");
+            h2d[k] = new_event();
+            fe_done[k] = new_event();
+        }
+        for (int i = 0; i < TR; i++) { c0[i] = timing_event(); c1[i] = timing_event(); }
+        rd = new Reader(o.in_path, bytes);
+    }
+    for (long long b = 0;; b++) {
+        const uint8_t* src = nullptr;
+        size_t stride = row;
+        if (dev_in) {
+            if (b >= o.nblocks) break;
+            src = o.d_iq + (size_t)b * o.block_stride;
+            stride = o.row_stride;
+        } else {
+            const int slot = rd->next();
+            if (slot < 0) break;
+            const int k = (int)(b & 1);
+            if (b >= 2) check_hip(hipStreamWaitEvent(sh->s_copy, fe_done[k], 0), "hipStreamWaitEvent");
+            harvest(b - TR + 1, true);                      // the ring slot this block reuses
+            harvest(b, false);
+            const int t = (int)(b % TR);
+            check_hip(hipEventRecord(c0[t], sh->s_copy), "hipEventRecord");
+            check_hip(hipMemcpyAsync(d_iq[k], rd->slot[slot], bytes, hipMemcpyHostToDevice, sh->s_copy), "hipMemcpyAsync");
+            check_hip(hipEventRecord(c1[t], sh->s_copy), "hipEventRecord");
+            check_hip(hipEventRecord(h2d[k], sh->s_copy), "hipEventRecord");
+            rd->release(slot, sh->s_copy);
+            check_hip(hipStreamWaitEvent(s, h2d[k], 0), "hipStreamWaitEvent");
+            src = d_iq[k];
+        }
+        if (b == 1) sh->t_block1 = std::chrono::steady_clock::now();
+        check_sdr(sdr_frontend(ctx, src, stride, s), "sdr_frontend");
+        if (!dev_in) check_hip(hipEventRecord(fe_done[(int)(b & 1)], s), "hipEventRecord");
+        FmBatch* fb = sh->q.acquire();
+        for (auto& e : fb->released) check_hip(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
+        check_sdr(sdr_get_fm_demod(ctx, fb->d_fm, fb->stride, s), "sdr_get_fm_demod");
+        check_hip(hipEventRecord(fb->ready, s), "hipEventRecord");
+        fb->block = b;
+        sh->q.push(fb);                                     // rffrontend.cpp:74
+        sh->blocks = b + 1;
+    }
+    sh->q.push(nullptr);                                    // end of stream
+    check_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (!dev_in) {
+        harvest(sh->blocks, true);
+        sh->read_s = rd->read_s;
+        delete rd;
+        for (auto& p : d_iq) (void)hipFree(p);
+        for (int i = 0; i < TR; i++) { (void)hipEventDestroy(c0[i]); (void)hipEventDestroy(c1[i]); }
+    }
+}
+
+// consumer prologue: the batch into this thread's context (wait_and_pop + prepare, async)
+bool consume(Shared* sh, sdr_ctx* ctx, int indicator) {
+    FmBatch* fb = nullptr;
+    sh->q.wait_and_pop(fb, indicator);
+    if (!fb) return false;
+    hipStream_t s = sh->s_fe;
+    check_hip(hipStreamWaitEvent(s, fb->ready, 0), "hipStreamWaitEvent");
+    check_sdr(sdr_push_fm_demod(ctx, fb->d_fm, fb->stride, s), "sdr_push_fm_demod");
+    check_hip(hipEventRecord(fb->released[indicator], s), "hipEventRecord");
+    sh->q.prepare(indicator);
+    return true;
+}
+
+// the consumer's PLL of the block whose pre part is on s_fe: signal + wait on s_post (persistent),
+// or one dispatch on its own stream between two events
+void consumer_pll(Shared* sh, sdr_ctx* ctx, int indicator, hipEvent_t pre, hipEvent_t pll) {
+    if (sh->persistent) {
+        check_sdr(sdr_plls_signal(ctx, sh->s_fe), "sdr_plls_signal");
+        check_sdr(sdr_plls_wait(ctx, sh->s_post), "sdr_plls_wait");
+        return;
+    }
+    check_hip(hipEventRecord(pre, sh->s_fe), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(sh->s_pll[indicator], pre, 0), "hipStreamWaitEvent");
+    if (indicator == 0) check_sdr(sdr_stereo_pll(ctx, sh->s_pll[0]), "sdr_stereo_pll");
+    else check_sdr(sdr_rds_pll(ctx, sh->s_pll[1]), "sdr_rds_pll");
+    check_hip(hipEventRecord(pll, sh->s_pll[indicator]), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(sh->s_post, pll, 0), "hipStreamWaitEvent");
+}
+
+// ------------------------------------------------------------------ audio (consumer 0)
+void audio_thread(Shared* sh) {
+    const sdr_multi_opts& o = sh->o;
+    check_hip(hipSetDevice(o.device), "hipSetDevice");
+    sdr_ctx* ctx = sh->ctx[1];
+    const size_t n = 2 * (size_t)sh->info.n_audio, bytes = n * o.nch * sizeof(int16_t);
+    hipStream_t s = sh->s_post;
+    hipEvent_t pre = new_event(), pll = new_event(), out_ready[2] = {new_event(), new_event()};
+    hipEvent_t d0[2] = {timing_event(), timing_event()}, d1[2] = {timing_event(), timing_event()};
+    int16_t *d_lr[2] = {}, *h_lr[2] = {};
+    for (int k = 0; k < 2; k++) {
+        check_hip(hipMalloc(reinterpret_cast<void**>(&d_lr[k]), bytes), "hipMalloc");
+        check_hip(hipHostMalloc(reinterpret_cast<void**>(&h_lr[k]), bytes, hipHostMallocDefault), "hipHostMalloc");
+    }
+    FILE* f = nullptr;
+    if (o.out_prefix) {
+        f = std::fopen((std::string(o.out_prefix) + ".pcm").c_str(), "wb");
+        if (!f) die(std::string("cannot write ") + o.out_prefix + ".pcm");
+    }
+    long long b = 0;
+    auto write_block = [&](long long blk) {   // stereo.cpp:111, for every channel
+        const int k = (int)(blk & 1);
+        check_hip(hipEventSynchronize(out_ready[k]), "hipEventSynchronize");
+        sh->d2h_ms += elapsed_ms(d0[k], d1[k]);
+        if (f) std::fwrite(h_lr[k], 1, bytes, f);
+        if (o.cap_lr && blk < o.cap_blocks)
+            for (int i = 0; i < o.ncap; i++)
+                std::memcpy(o.cap_lr + ((size_t)blk * o.ncap + i) * n, h_lr[k] + (size_t)o.cap_ch[i] * n,
+                            n * sizeof(int16_t));
+    };
+    while (consume(sh, ctx, 0)) {
+        const int k = (int)(b & 1);
+        check_sdr(sdr_stereo_pre(ctx, sh->s_fe), "sdr_stereo_pre");
+        consumer_pll(sh, ctx, 0, pre, pll);
+        check_sdr(sdr_stereo_post(ctx, d_lr[k], n, s), "sdr_stereo_post");
+        check_hip(hipEventRecord(d0[k], s), "hipEventRecord");
+        check_hip(hipMemcpyAsync(h_lr[k], d_lr[k], bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+        check_hip(hipEventRecord(d1[k], s), "hipEventRecord");
+        check_hip(hipEventRecord(out_ready[k], s), "hipEventRecord");
+        if (b >= 1) write_block(b - 1);                     // overlaps block b's GPU work
+        b++;
+    }
+    if (b >= 1) write_block(b - 1);
+    if (f) std::fclose(f);
+    check_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+    for (int k = 0; k < 2; k++) {
+        (void)hipFree(d_lr[k]);
+        (void)hipHostFree(h_lr[k]);
+    }
+}
+
+// ------------------------------------------------------------------ RDS (consumer 1)
+struct FrameState {   // rds.cpp:67-92, per channel
+    uint64_t reg = 0, chars = 0, output = 0;
+    bool first_time = true;
+    int decoder_cont = 0;
+    unsigned int idx = 0;
+    std::deque<std::string> window;
+    std::vector<int> stream, stream_state;
+    std::string text;
+};
+
+void rds_thread(Shared* sh) {
+    const sdr_multi_opts& o = sh->o;
+    check_hip(hipSetDevice(o.device), "hipSetDevice");
+    sdr_ctx* ctx = sh->ctx[2];
+    hipStream_t s = sh->s_post;
+    hipEvent_t pre = new_event(), pll = new_event(), out_ready[2] = {new_event(), new_event()};
+    int32_t *d_nbits = nullptr, *h_nbits[2] = {};
+    uint8_t *d_bits = nullptr, *h_bits[2] = {};
+    check_hip(hipMalloc(reinterpret_cast<void**>(&d_nbits), o.nch * sizeof(int32_t)), "hipMalloc");
+    check_hip(hipMalloc(reinterpret_cast<void**>(&d_bits), (size_t)o.nch * SDR_MAX_BITS), "hipMalloc");
+    for (int k = 0; k < 2; k++) {
+        check_hip(hipHostMalloc(reinterpret_cast<void**>(&h_nbits[k]), o.nch * sizeof(int32_t), hipHostMallocDefault),
+                  "hipHostMalloc");
+        check_hip(hipHostMalloc(reinterpret_cast<void**>(&h_bits[k]), (size_t)o.nch * SDR_MAX_BITS,
+                                hipHostMallocDefault), "hipHostMalloc");
+    }
+    std::vector<FrameState> fs((size_t)o.nch);
+    auto frame_layer = [&](long long blk) {   // rds.cpp:181-189 per channel; parse() prints to cerr
+        const int k = (int)(blk & 1);
+        check_hip(hipEventSynchronize(out_ready[k]), "hipEventSynchronize");
+        if (o.cap_nbits && blk < o.cap_blocks)
+            for (int i = 0; i < o.ncap; i++) {
+                o.cap_nbits[(size_t)blk * o.ncap + i] = h_nbits[k][o.cap_ch[i]];
+                std::memcpy(o.cap_bits + ((size_t)blk * o.ncap + i) * SDR_MAX_BITS,
+                            h_bits[k] + (size_t)o.cap_ch[i] * SDR_MAX_BITS, SDR_MAX_BITS);
+            }
+        if (!o.out_prefix) return;
+        std::streambuf* saved = std::cerr.rdbuf();
+        for (int c = 0; c < o.nch; c++) {
+            const int nb = h_nbits[k][c];
+            if (nb < 0) continue;                       // block_count <= 5 (rds.cpp:135)
+            FrameState& st = fs[(size_t)c];
+            const uint8_t* bits = h_bits[k] + (size_t)c * SDR_MAX_BITS;
+            st.decoder_cont++;
+            st.stream.insert(st.stream.end(), bits, bits + nb);
+            if (st.decoder_cont == 15) {
+                std::ostringstream text;
+                std::cerr.rdbuf(text.rdbuf());
+                start_frame_sync(st.idx, st.stream, st.stream_state, st.reg, st.chars, st.output, st.first_time,
+                                 st.window);
+                std::cerr.rdbuf(saved);
+                st.text += text.str();
+                st.decoder_cont = 0;
+                st.idx = 0;
+                st.stream.clear();
+            }
+        }
+    };
+    long long b = 0;
+    while (consume(sh, ctx, 1)) {
+        const int k = (int)(b & 1);
+        check_sdr(sdr_rds_pre(ctx, sh->s_fe), "sdr_rds_pre");
+        consumer_pll(sh, ctx, 1, pre, pll);
+        check_sdr(sdr_rds_post(ctx, nullptr, 0, s), "sdr_rds_post");
+        check_sdr(sdr_rds_bits(ctx, nullptr, nullptr, nullptr, 0, d_nbits, d_bits, SDR_MAX_BITS, s), "sdr_rds_bits");
+        check_hip(hipMemcpyAsync(h_nbits[k], d_nbits, o.nch * sizeof(int32_t), hipMemcpyDeviceToHost, s),
+                  "hipMemcpyAsync");
+        check_hip(hipMemcpyAsync(h_bits[k], d_bits, (size_t)o.nch * SDR_MAX_BITS, hipMemcpyDeviceToHost, s),
+                  "hipMemcpyAsync");
+        check_hip(hipEventRecord(out_ready[k], s), "hipEventRecord");
+        if (b >= 1) frame_layer(b - 1);
+        b++;
+    }
+    if (b >= 1) frame_layer(b - 1);
+    if (o.out_prefix) {
+        FILE* f = std::fopen((std::string(o.out_prefix) + ".rds").c_str(), "w");
+        if (!f) die(std::string("cannot write ") + o.out_prefix + ".rds");
+        for (int c = 0; c < o.nch; c++) {
+            std::istringstream lines(fs[(size_t)c].text);
+            for (std::string line; std::getline(lines, line);) std::fprintf(f, "ch %d: %s\n", c, line.c_str());
+        }
+        std::fclose(f);
+    }
+    check_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+    (void)hipFree(d_nbits);
+    (void)hipFree(d_bits);
+    for (int k = 0; k < 2; k++) {
+        (void)hipHostFree(h_nbits[k]);
+        (void)hipHostFree(h_bits[k]);
+    }
+}
+
+// device-clock period per block of a finished persistent launch, blocks 1 .. last (ms)
+double launch_period_ms(sdr_ctx* ctx, hipStream_t s) {
+    std::vector<unsigned long long> t0(65536), t1(65536);
+    int nb = 0;
+    check_sdr(sdr_plls_timeline(ctx, t0.data(), t1.data(), (int)t0.size(), &nb, s), "sdr_plls_timeline");
+    if (nb < 2) return 0.0;
+    return (double)(t1[(size_t)nb - 1] - t1[0]) / (double)(nb - 1) / 1e5;   // 100 MHz ticks
+}
+
+long long regular_file_blocks(const char* path, size_t block_bytes) {
+    if (!path || std::strcmp(path, "-") == 0) return -1;
+    struct stat sb;
+    if (::stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) return -1;
+    return (long long)((size_t)sb.st_size / block_bytes);
+}
+
+}  // namespace
+
+extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats) {
+    if (!opts || opts->nch <= 0 || (!opts->in_path && (!opts->d_iq || opts->nblocks <= 0)))
+        return SDR_E_INVALID;
+    Shared sh;
+    sh.o = *opts;
+    const sdr_multi_opts& o = sh.o;
+    check_hip(hipSetDevice(o.device), "hipSetDevice");
+    check_sdr(sdr_ctx_create(&sh.ctx[0], o.device, o.nch, o.mode, 0, o.flags), "sdr_ctx_create");
+    check_sdr(sdr_ctx_create(&sh.ctx[1], o.device, o.nch, o.mode, 0, o.flags), "sdr_ctx_create");
+    check_sdr(sdr_ctx_create(&sh.ctx[2], o.device, o.nch, o.mode, 1, o.flags), "sdr_ctx_create");
+    check_sdr(sdr_ctx_info(sh.ctx[0], &sh.info), "sdr_ctx_info");
+    const size_t row = 2 * (size_t)sh.info.block_iq;
+    if (!o.in_path && o.row_stride < row) return SDR_E_INVALID;
+    sh.nblocks_known = o.in_path ? regular_file_blocks(o.in_path, row * o.nch) : o.nblocks;
+    // streams: the PLLs on [0, pll_cus) (halves), everything else on the rest
+    const int half = o.pll_cus / 2;
+    if (half > 0) {
+        sh.s_fe = masked_stream(o.device, 0, o.pll_cus, 1);
+        sh.s_post = masked_stream(o.device, 0, o.pll_cus, 1);
+        sh.s_pll[0] = masked_stream(o.device, 0, half, 0);
+        sh.s_pll[1] = masked_stream(o.device, half, half, 0);
+        sh.persistent = sh.nblocks_known > 0;
+        for (int i = 0; i < 2 && sh.persistent; i++) {   // the library's residency rule (sdr_plls_fits)
+            int waves = 0;
+            long long groups = 0, resident = 0;
+            check_sdr(sdr_plls_fits(sh.ctx[1 + i], i == 0 ? SDR_PLLS_STEREO : SDR_PLLS_RDS, i * half, half, &waves,
+                                    &groups, &resident), "sdr_plls_fits");
+            sh.persistent = groups <= resident;
+        }
+    } else {
+        sh.s_fe = plain_stream();
+        sh.s_post = plain_stream();
+        sh.s_pll[0] = plain_stream();
+        sh.s_pll[1] = plain_stream();
+    }
+    if (o.in_path) sh.s_copy = plain_stream();
+    // two recycled device batches of fm_demod [nch][block_if] (threadsafequeue.h's one slot, plus the
+    // one the producer fills meanwhile)
+    std::vector<FmBatch> batches(2);
+    for (auto& fb : batches) {
+        fb.nch = o.nch;
+        fb.n = sh.info.block_if;
+        fb.stride = (size_t)(fb.n + 63) / 64 * 64;
+        check_hip(hipMalloc(reinterpret_cast<void**>(&fb.d_fm), fb.stride * o.nch * sizeof(float)), "hipMalloc");
+        fb.ready = new_event();
+        for (auto& e : fb.released) {
+            e = new_event();
+            check_hip(hipEventRecord(e, nullptr), "hipEventRecord");   // trivially complete
+        }
+        sh.q.add_free(&fb);
+    }
+    check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    // one persistent launch per consumer for every block (before the first sdr_push_fm_demod)
+    if (sh.persistent) {
+        check_sdr(sdr_plls_launch_sel(sh.ctx[1], (int)sh.nblocks_known, SDR_PLLS_STEREO, sh.s_pll[0]), "sdr_plls_launch_sel");
+        check_sdr(sdr_plls_launch_sel(sh.ctx[2], (int)sh.nblocks_known, SDR_PLLS_RDS, sh.s_pll[1]), "sdr_plls_launch_sel");
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    std::thread t_rds(rds_thread, &sh);      // project.cpp:134-136
+    std::thread t_audio(audio_thread, &sh);
+    std::thread t_rf(rf_thread, &sh);
+    t_rf.join();
+    t_audio.join();
+    t_rds.join();
+    const auto t_end = std::chrono::steady_clock::now();
+    sdr_multi_stats st{};
+    st.blocks = sh.blocks;
+    st.seconds = std::chrono::duration<double>(t_end - t0).count();
+    st.steady_seconds = sh.blocks >= 2 ? std::chrono::duration<double>(t_end - sh.t_block1).count() : 0.0;
+    st.read_s = sh.read_s;
+    st.h2d_ms = sh.h2d_ms;
+    st.d2h_ms = sh.d2h_ms;
+    st.persistent = sh.persistent ? 1 : 0;
+    if (sh.persistent) {
+        if (sh.blocks != sh.nblocks_known) die("sdr_multi: fewer blocks than the persistent launches cover");
+        for (int i = 0; i < 2; i++) {
+            double ms[1] = {0.0};
+            int nb = 0;
+            check_sdr(sdr_plls_report(sh.ctx[1 + i], ms, 0, &nb, sh.s_pll[i]), "sdr_plls_report");   // a timeout fails here
+            st.pll_period_ms = std::max(st.pll_period_ms, launch_period_ms(sh.ctx[1 + i], sh.s_pll[i]));
+        }
+    }
+    check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    for (auto& fb : batches) {
+        (void)hipFree(fb.d_fm);
+        (void)hipEventDestroy(fb.ready);
+        for (auto& e : fb.released) (void)hipEventDestroy(e);
+    }
+    for (sdr_ctx* c : sh.ctx) sdr_ctx_destroy(c);
+    for (hipStream_t s : {sh.s_fe, sh.s_post, sh.s_pll[0], sh.s_pll[1]}) {
+        if (half > 0) (void)sdr_stream_destroy(s);
+        else (void)hipStreamDestroy(s);
+    }
+    if (sh.s_copy) (void)hipStreamDestroy(sh.s_copy);
+    if (stats) *stats = st;
+    return SDR_OK;
+}

@@ -24,6 +24,17 @@ def test_library_exports_every_declared_symbol(pkg):
     assert not missing, missing
 
 
+def test_host_library_exports_the_multi_receiver_engine():
+    """include/sdr_multi.h's entry point lives in libsdr_host.so (the engine behind sdr_multi and the
+    bench's queue_plumbed leg); it rejects a NULL options block without touching a GPU."""
+    host = C.CDLL(str(ROOT / "real-time-sdr_amd" / "libsdr_host.so"))
+    names = _declared("sdr_multi.h")
+    assert names == ["sdr_multi_run"]
+    assert all(hasattr(host, n) for n in names)
+    host.sdr_multi_run.argtypes = [C.c_void_p, C.c_void_p]
+    assert host.sdr_multi_run(None, None) == -1
+
+
 def test_errors_are_status_codes(pkg):
     lib = pkg.lib()
     assert lib.sdr_version() >= 1
