@@ -186,7 +186,7 @@ template <int NT, bool SQUARE, bool PK = false>
 __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, size_t x_stride,
                                                 const float* __restrict__ hist, size_t hist_stride, int ny,
                                                 const FirRb f) {
-    static_assert(!PK || NT == 3, "packed pairs: sets 0 and 1 of a 3-set pass");
+    static_assert(!PK || NT >= 2, "packed pairs: sets 0 and 1 of a 2- or 3-set pass");
     constexpr int T = FRB_T, R = FRB_R;
     __shared__ __attribute__((aligned(16))) float sx[(FRB_W + 3) & ~3];
     __shared__ uint32_t s_poison;                                 // one decision per workgroup
@@ -234,17 +234,19 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
     typedef float f4v __attribute__((ext_vector_type(FRB_TC)));
     if constexpr (PK) {
         typedef float f8v __attribute__((ext_vector_type(2 * FRB_TC)));
+        constexpr bool S2 = NT == 3;                     // a third, scalar set beside the pair
         f32x2 a01[R];
         float a2[R];
 #pragma unroll
         for (int j = 0; j < R; j++) { a01[j] = f32x2{0.0f, 0.0f}; a2[j] = 0.0f; }
         f8v pb[2];                                       // {h0, h1} pairs of chunk c in pb[c & 1]
-        f4v sb[2];                                       // set 2's taps of chunk c
+        f4v sb[2] = {};                                  // set 2's taps of chunk c
         auto load8 = [&](f8v& d, int c) {
             asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(d) : "s"(f.h01), "s"(c * FRB_TC * 8) : "memory");
         };
         auto load4 = [&](f4v& d, int c) {
-            asm volatile("s_load_dwordx4 %0, %1, %2" : "=s"(d) : "s"(f.h[2]), "s"(c * FRB_TC * 4) : "memory");
+            if constexpr (S2)
+                asm volatile("s_load_dwordx4 %0, %1, %2" : "=s"(d) : "s"(f.h[NT - 1]), "s"(c * FRB_TC * 4) : "memory");
         };
         load8(pb[0], 0);
         load4(sb[0], 0);
@@ -266,7 +268,7 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
                         // inline-asm v_pk_mul_f32)
                         const f32x2 pr = __builtin_bit_cast(f32x2, hp) * f32x2{w[i], w[i]};
                         a01[j] = a01[j] + pr;                                  // filter.cpp:115
-                        a2[j] = a2[j] + sb[c & 1][kk] * w[i];
+                        if constexpr (S2) a2[j] = a2[j] + sb[c & 1][kk] * w[i];
                     }
                 }
                 if (kk == 0 && c + 1 < FRB_NC) {
@@ -283,7 +285,11 @@ __global__ __launch_bounds__(BLK) void k_fir_rb(const float* __restrict__ x, siz
             }
         }
 #pragma unroll
-        for (int j = 0; j < R; j++) { a[0][j] = a01[j].x; a[1][j] = a01[j].y; a[NT - 1][j] = a2[j]; }
+        for (int j = 0; j < R; j++) {
+            a[0][j] = a01[j].x;
+            a[1][j] = a01[j].y;
+            if constexpr (S2) a[NT - 1][j] = a2[j];
+        }
     } else {
 #pragma unroll
     for (int t = 0; t < NT; t++)
@@ -1118,6 +1124,50 @@ __global__ void k_hist_copy(float* __restrict__ y, const float* __restrict__ y_o
     const int ch = blockIdx.x;
     for (int i = threadIdx.x; i < HIST; i += blockDim.x)
         y[(size_t)ch * stride + i - HIST] = y_other[(size_t)ch * stride + n - HIST + i];
+}
+
+// Rows [nch][n] f32 from src to dst, and with hist_other the HIST samples in front of each dst row
+// from the end of hist_other's row (the extended-stream history, as k_hist_copy): one pass at HBM
+// rate (16-byte vectors when both rows are 16-byte aligned), where hipMemcpy2DAsync's rectangle blit
+// moved the 30 MB of a 1024-channel fm_demod block at ~2 TB/s (31.8 us, profiles/r06/queue/).
+constexpr int CR_BLK = 256, CR_V = 4;    // threads per workgroup, float4s per thread
+__global__ __launch_bounds__(CR_BLK) void k_copy_rows(float* __restrict__ dst, size_t dst_stride,
+                                                       const float* __restrict__ src, size_t src_stride, int n,
+                                                       const float* __restrict__ hist_other, int vec) {
+    const int ch = blockIdx.y;
+    float* d = dst + (size_t)ch * dst_stride;
+    const float* a = src + (size_t)ch * src_stride;
+    if (hist_other && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < HIST; i += CR_BLK) d[i - HIST] = hist_other[(size_t)ch * dst_stride + n - HIST + i];
+    const int i0 = blockIdx.x * CR_BLK * CR_V * 4;   // first float of this workgroup
+    if (vec) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        f4* d4 = reinterpret_cast<f4*>(d + i0);
+        const f4* a4 = reinterpret_cast<const f4*>(a + i0);
+        f4 v[CR_V];
+#pragma unroll
+        for (int u = 0; u < CR_V; u++) {
+            const int i = i0 + 4 * (threadIdx.x + u * CR_BLK);
+            if (i + 3 < n) v[u] = __builtin_nontemporal_load(a4 + threadIdx.x + u * CR_BLK);
+        }
+#pragma unroll
+        for (int u = 0; u < CR_V; u++) {
+            const int i = i0 + 4 * (threadIdx.x + u * CR_BLK);
+            if (i + 3 < n) d4[threadIdx.x + u * CR_BLK] = v[u];
+            else for (int k = i; k < n && k < i + 4; k++) d[k] = a[k];
+        }
+    } else {
+        for (int i = i0 + threadIdx.x; i < min(n, i0 + CR_BLK * CR_V * 4); i += CR_BLK) d[i] = a[i];
+    }
+}
+int copy_rows(float* dst, size_t dst_stride, const float* src, size_t src_stride, int n, int nch,
+              const float* hist_other, hipStream_t s) {
+    const int vec = (reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+                     dst_stride % 4 == 0 && src_stride % 4 == 0) ? 1 : 0;
+    hipLaunchKernelGGL(k_copy_rows, dim3(cdiv(n, CR_BLK * CR_V * 4), nch), dim3(CR_BLK), 0, s, dst, dst_stride, src,
+                       src_stride, n, hist_other, vec);
+    LAUNCH_CHECK();
+    return SDR_OK;
 }
 
 // state <- last nstate of x (filter.cpp:119 / :145) for the primitive entry points
@@ -2166,9 +2216,7 @@ int sdr_get_fm_demod(sdr_ctx* c, float* fm, size_t fm_stride, void* stream) {
     if (const int rf_ = check_failed(c, "get_fm_demod")) return rf_;
     if (c->block < 0) return fail(SDR_E_INVALID, "no block processed yet");
     const sdr_info& in = c->info;
-    HIP_TRY(hipMemcpy2DAsync(fm, fm_stride * sizeof(float), c->fm_cur(), c->fm_stride * sizeof(float),
-                             in.block_if * sizeof(float), c->nch, hipMemcpyDeviceToDevice, S(stream)));
-    return SDR_OK;
+    return copy_rows(fm, fm_stride, c->fm_cur(), c->fm_stride, in.block_if, c->nch, nullptr, S(stream));
 }
 
 int sdr_mono(sdr_ctx* c, int16_t* audio, size_t audio_stride, void* stream) {
@@ -2219,10 +2267,10 @@ int fir_rb(const sdr_ctx* c, const float* x, size_t x_stride, int n, FirRb f, hi
            int xn = 0) {
     if (xn <= 0) { x0 = 0; xn = cdiv(n, FRB_TILE); }
     f.x0 = x0;
-    // the 3-set pass with its first two sets as packed pairs
-    if constexpr (NT == 3 && !SQUARE) {
+    // the 2- and 3-set passes with their first two sets (pilot, band) as packed pairs
+    if constexpr (NT >= 2 && !SQUARE) {
         if (f.h01) {
-            hipLaunchKernelGGL((k_fir_rb<3, false, true>), dim3(xn, c->nch), dim3(BLK), 0, s, x,
+            hipLaunchKernelGGL((k_fir_rb<NT, false, true>), dim3(xn, c->nch), dim3(BLK), 0, s, x,
                                x_stride, x, x_stride, n, f);
             LAUNCH_CHECK();
             return SDR_OK;
@@ -2244,6 +2292,7 @@ FirRb stereo_fir(sdr_ctx* c) {
     f.rx0 = c->rxbuf(c->rx_st);
     f.rx_stride = c->plain_stride;
     f.y0neg = c->plain(c->pilot_neg);
+    f.h01 = c->pilot_band_h;     // the pair as packed f32 (k_fir_rb<2, false, true>)
     return f;
 }
 }  // namespace
@@ -3088,11 +3137,9 @@ int sdr_push_fm_demod(sdr_ctx* c, const float* fm, size_t fm_stride, void* strea
     const int p = c->parity ^ 1;
     float* dst = c->fm + p * c->fm_par;
     if (const int rw = release_wait(c, p, REL_MONO | REL_STEREO, S(stream))) return rw;
-    HIP_TRY(hipMemcpy2DAsync(dst, c->fm_stride * sizeof(float), fm, fm_stride * sizeof(float),
-                             in.block_if * sizeof(float), c->nch, hipMemcpyDeviceToDevice, S(stream)));
-    hipLaunchKernelGGL(k_hist_copy, dim3(c->nch), dim3(HIST), 0, S(stream), dst, c->fm + (p ^ 1) * c->fm_par,
-                       c->fm_stride, in.block_if);
-    LAUNCH_CHECK();
+    if (const int r = copy_rows(dst, c->fm_stride, fm, fm_stride, in.block_if, c->nch, c->fm + (p ^ 1) * c->fm_par,
+                                S(stream)))
+        return r;
     c->parity = p;
     c->block++;
     return SDR_OK;
