@@ -178,7 +178,11 @@ class GpuStepper:
         self.args, self.nch, self.nblocks, self.first = args, nch, nblocks, first
         self.dev = dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
-        self.iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
+        # SDR_BENCH_INPUT_LAST=1 (A/B): generate the input at the end of the set-up, right before the
+        # warm-up, instead of first
+        self.input_last = os.environ.get("SDR_BENCH_INPUT_LAST", "0") == "1"
+        if not self.input_last:
+            self.iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
         fast = args.numerics == "fast"
         self.fast = fast
         self.pipe = pkg.Pipeline(nch, mode=0, rds_on=True, device=local,
@@ -251,6 +255,8 @@ class GpuStepper:
         self.gather_done = [ev() for _ in range(nblocks)]
         self.pre_done, self.post_done = [tev() for _ in range(nblocks)], [tev() for _ in range(nblocks)]
         self.post_dsp_done = [ev() for _ in range(nblocks)]   # block b's post DSP (before its captures)
+        if self.input_last:
+            self.iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
         # the front end of block b also waits for block b-2's whole post stream work (the RDS chain
         # after its mixer, the output copies and captures included), not only for the library's own
         # parity release (its readers' first kernels): the front end then runs beside the PLL alone
