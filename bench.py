@@ -178,9 +178,11 @@ class GpuStepper:
         self.args, self.nch, self.nblocks, self.first = args, nch, nblocks, first
         self.dev = dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
-        # SDR_BENCH_INPUT_LAST=1 (A/B): generate the input at the end of the set-up, right before the
-        # warm-up, instead of first
-        self.input_last = os.environ.get("SDR_BENCH_INPUT_LAST", "0") == "1"
+        # the input is generated at the end of the set-up, right before the warm-up, so the GPU goes
+        # from that load into the warm-up without the set-up's idle gap (shader clock 2306-2320 ->
+        # 2312-2325 MHz, 0.7057-0.7076 -> 0.7032-0.7063 ms per step over 3 interleaved pairs at the
+        # driver's 20/5, profiles/r06/input_last_ab.txt); SDR_BENCH_INPUT_LAST=0: first, as before
+        self.input_last = os.environ.get("SDR_BENCH_INPUT_LAST", "1") == "1"
         if not self.input_last:
             self.iq = make_input(torch, nch, nblocks, first_channel=first, device=dev)
         fast = args.numerics == "fast"
@@ -1188,7 +1190,8 @@ def _multi_structs():
 
     class Stats(C.Structure):
         _fields_ = [("blocks", C.c_longlong), ("seconds", C.c_double), ("steady_seconds", C.c_double),
-                    ("pll_period_ms", C.c_double), ("read_s", C.c_double), ("h2d_ms", C.c_double),
+                    ("pll_period_ms", C.c_double), ("pll_span_ms", C.c_double), ("read_s", C.c_double),
+                    ("h2d_ms", C.c_double),
                     ("d2h_ms", C.c_double), ("persistent", C.c_int)]
     return Opts, Stats
 
@@ -1229,7 +1232,7 @@ def queue_child(a) -> None:
     import hashlib
     iq_sha = hashlib.sha256(np.ascontiguousarray(iq[:, ch].cpu().numpy()).tobytes()).hexdigest()
     print(json.dumps({"iq_sha": iq_sha, "blocks": st.blocks, "seconds": st.seconds, "steady_seconds": st.steady_seconds,
-                      "pll_period_ms": st.pll_period_ms, "d2h_ms": st.d2h_ms, "persistent": st.persistent,
+                      "pll_period_ms": st.pll_period_ms, "pll_span_ms": st.pll_span_ms, "d2h_ms": st.d2h_ms, "persistent": st.persistent,
                       "block_iq": info.block_iq}), flush=True)
 
 
@@ -1275,6 +1278,7 @@ def queue_plumbed_leg(args, st, nch: int) -> dict:
         "steady_value": (round((q["blocks"] - 1) * samples / q["steady_seconds"] / 1e6, 2)
                          if q["steady_seconds"] else None),
         "pll_period_ms": round(q["pll_period_ms"], 4),
+        "outside_pll_span_ms": round(q["seconds"] * 1e3 - q["pll_span_ms"], 3),
         "pll": "persistent" if q["persistent"] else "per-block dispatch",
         "d2h_ms": round(q["d2h_ms"], 2),
         "outputs_equal_to_bench_capture": bool(equal),

@@ -50,6 +50,7 @@ typedef struct sdr_multi_stats {
     double steady_seconds;        /* the same from block 1's front end on (block 0's fill excluded) */
     double pll_period_ms;         /* persistent mode: device-clock period per block of the slower
                                      consumer's PLL launch, blocks 1 .. last (0 in dispatch mode) */
+    double pll_span_ms;           /* persistent mode: block 0's PLL start to the last block's end */
     double read_s, h2d_ms, d2h_ms;   /* byte-stream input: read time, GPU time of the uploads; L/R D2H */
     int persistent;               /* 1: persistent PLL launches, 0: per-block dispatches */
 } sdr_multi_stats;

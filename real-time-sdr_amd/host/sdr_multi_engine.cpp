@@ -213,13 +213,30 @@ struct Shared {
     std::chrono::steady_clock::time_point t_block1{};  // block 1's front end enqueued
 };
 
+// the host waits for a block's outputs by polling the event (yielding between polls) rather than
+// hipEventSynchronize, so a waiting consumer thread never sits inside the runtime while the other
+// threads enqueue the next blocks (SDR_MULTI_SYNC=event: hipEventSynchronize, for A/B)
+bool g_poll_events = true;
+void wait_event(hipEvent_t e) {
+    if (!g_poll_events) {
+        check_hip(hipEventSynchronize(e), "hipEventSynchronize");
+        return;
+    }
+    for (;;) {
+        const hipError_t r = hipEventQuery(e);
+        if (r == hipSuccess) return;
+        if (r != hipErrorNotReady) check_hip(r, "hipEventQuery");
+        std::this_thread::yield();
+    }
+}
+
 hipEvent_t timing_event() {
     hipEvent_t e = nullptr;
     check_hip(hipEventCreate(&e), "hipEventCreate");
     return e;
 }
 float elapsed_ms(hipEvent_t a, hipEvent_t b) {
-    check_hip(hipEventSynchronize(b), "hipEventSynchronize");
+    wait_event(b);
     float ms = 0.0f;
     check_hip(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
     return ms;
@@ -348,7 +365,7 @@ void audio_thread(Shared* sh) {
     long long b = 0;
     auto write_block = [&](long long blk) {   // stereo.cpp:111, for every channel
         const int h = (int)(blk % NH);
-        check_hip(hipEventSynchronize(r.out_ready[h]), "hipEventSynchronize");
+        wait_event(r.out_ready[h]);
         sh->d2h_ms += elapsed_ms(r.d0[h], r.d1[h]);
         if (f) std::fwrite(r.h_lr[h], 1, bytes, f);
         if (o.cap_lr && blk < o.cap_blocks)
@@ -402,7 +419,7 @@ void rds_thread(Shared* sh) {
     std::vector<FrameState> fs((size_t)o.nch);
     auto frame_layer = [&](long long blk) {   // rds.cpp:181-189 per channel; parse() prints to cerr
         const int k = (int)(blk % NH);
-        check_hip(hipEventSynchronize(out_ready[k]), "hipEventSynchronize");
+        wait_event(out_ready[k]);
         if (o.cap_nbits && blk < o.cap_blocks)
             for (int i = 0; i < o.ncap; i++) {
                 o.cap_nbits[(size_t)blk * o.ncap + i] = h_nbits[k][o.cap_ch[i]];
@@ -506,13 +523,15 @@ void free_consumers(Shared* sh) {
     }
 }
 
-// device-clock period per block of a finished persistent launch, blocks 1 .. last (ms)
-double launch_period_ms(sdr_ctx* ctx, hipStream_t s) {
+// device-clock period per block of a finished persistent launch, blocks 1 .. last, and the span
+// from block 0's start to the last block's end (ms)
+void launch_period_ms(sdr_ctx* ctx, hipStream_t s, double* period, double* span) {
     std::vector<unsigned long long> t0(65536), t1(65536);
     int nb = 0;
     check_sdr(sdr_plls_timeline(ctx, t0.data(), t1.data(), (int)t0.size(), &nb, s), "sdr_plls_timeline");
-    if (nb < 2) return 0.0;
-    return (double)(t1[(size_t)nb - 1] - t1[0]) / (double)(nb - 1) / 1e5;   // 100 MHz ticks
+    if (nb < 2) return;
+    *period = std::max(*period, (double)(t1[(size_t)nb - 1] - t1[0]) / (double)(nb - 1) / 1e5);   // 100 MHz ticks
+    *span = std::max(*span, (double)(t1[(size_t)nb - 1] - t0[0]) / 1e5);
 }
 
 long long regular_file_blocks(const char* path, size_t block_bytes) {
@@ -584,6 +603,7 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
         check_sdr(sdr_plls_launch_sel(sh.ctx[1], (int)sh.nblocks_known, SDR_PLLS_STEREO, sh.s_pll[0]), "sdr_plls_launch_sel");
         check_sdr(sdr_plls_launch_sel(sh.ctx[2], (int)sh.nblocks_known, SDR_PLLS_RDS, sh.s_pll[1]), "sdr_plls_launch_sel");
     }
+    if (const char* e = std::getenv("SDR_MULTI_SYNC"); e && std::strcmp(e, "event") == 0) g_poll_events = false;
     const auto t0 = std::chrono::steady_clock::now();
     std::thread t_rds(rds_thread, &sh);      // project.cpp:134-136
     std::thread t_audio(audio_thread, &sh);
@@ -606,7 +626,7 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
             double ms[1] = {0.0};
             int nb = 0;
             check_sdr(sdr_plls_report(sh.ctx[1 + i], ms, 0, &nb, sh.s_pll[i]), "sdr_plls_report");   // a timeout fails here
-            st.pll_period_ms = std::max(st.pll_period_ms, launch_period_ms(sh.ctx[1 + i], sh.s_pll[i]));
+            launch_period_ms(sh.ctx[1 + i], sh.s_pll[i], &st.pll_period_ms, &st.pll_span_ms);
         }
     }
     check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
