@@ -42,6 +42,10 @@ typedef struct sdr_multi_opts {
     int16_t *cap_lr;
     int32_t *cap_nbits;
     uint8_t *cap_bits;
+    /* optional (NULL: none), persistent mode: each consumer's PLL end stamp of every block (100 MHz
+     * device clock), audio's at pll_end[b], RDS's at pll_end[stamp_blocks + b], b < stamp_blocks */
+    int stamp_blocks;
+    unsigned long long *pll_end;
 } sdr_multi_opts;
 
 typedef struct sdr_multi_stats {

@@ -525,10 +525,12 @@ void free_consumers(Shared* sh) {
 
 // device-clock period per block of a finished persistent launch, blocks 1 .. last, and the span
 // from block 0's start to the last block's end (ms)
-void launch_period_ms(sdr_ctx* ctx, hipStream_t s, double* period, double* span) {
+void launch_period_ms(sdr_ctx* ctx, hipStream_t s, double* period, double* span, unsigned long long* ends, int nends) {
     std::vector<unsigned long long> t0(65536), t1(65536);
     int nb = 0;
     check_sdr(sdr_plls_timeline(ctx, t0.data(), t1.data(), (int)t0.size(), &nb, s), "sdr_plls_timeline");
+    if (ends)
+        for (int b = 0; b < nends && b < nb; b++) ends[b] = t1[(size_t)b];
     if (nb < 2) return;
     *period = std::max(*period, (double)(t1[(size_t)nb - 1] - t1[0]) / (double)(nb - 1) / 1e5);   // 100 MHz ticks
     *span = std::max(*span, (double)(t1[(size_t)nb - 1] - t0[0]) / 1e5);
@@ -626,7 +628,8 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
             double ms[1] = {0.0};
             int nb = 0;
             check_sdr(sdr_plls_report(sh.ctx[1 + i], ms, 0, &nb, sh.s_pll[i]), "sdr_plls_report");   // a timeout fails here
-            launch_period_ms(sh.ctx[1 + i], sh.s_pll[i], &st.pll_period_ms, &st.pll_span_ms);
+            launch_period_ms(sh.ctx[1 + i], sh.s_pll[i], &st.pll_period_ms, &st.pll_span_ms,
+                             o.pll_end ? o.pll_end + (size_t)i * o.stamp_blocks : nullptr, o.stamp_blocks);
         }
     }
     check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
