@@ -206,6 +206,7 @@ struct Shared {
     ThreadSafeQueue<FmBatch*> q;
     sdr_ctx* ctx[3] = {};                // RF, audio, RDS (each thread owns its context)
     hipStream_t s_fe = nullptr, s_post = nullptr, s_pll[2] = {}, s_copy = nullptr;
+    hipStream_t s_post_c[2] = {};        // consumer i's post stream: s_post, or its own (SDR_MULTI_POSTS=2)
     bool persistent = false;
     long long nblocks_known = -1;        // -1: a byte stream of unknown length
     long long blocks = 0;
@@ -338,7 +339,7 @@ bool consume(Shared* sh, sdr_ctx* ctx, int indicator) {
 void consumer_pll(Shared* sh, sdr_ctx* ctx, int indicator, hipEvent_t pre, hipEvent_t pll) {
     if (sh->persistent) {
         check_sdr(sdr_plls_signal(ctx, sh->s_fe), "sdr_plls_signal");
-        check_sdr(sdr_plls_wait(ctx, sh->s_post), "sdr_plls_wait");
+        check_sdr(sdr_plls_wait(ctx, sh->s_post_c[indicator]), "sdr_plls_wait");
         return;
     }
     check_hip(hipEventRecord(pre, sh->s_fe), "hipEventRecord");
@@ -346,7 +347,7 @@ void consumer_pll(Shared* sh, sdr_ctx* ctx, int indicator, hipEvent_t pre, hipEv
     if (indicator == 0) check_sdr(sdr_stereo_pll(ctx, sh->s_pll[0]), "sdr_stereo_pll");
     else check_sdr(sdr_rds_pll(ctx, sh->s_pll[1]), "sdr_rds_pll");
     check_hip(hipEventRecord(pll, sh->s_pll[indicator]), "hipEventRecord");
-    check_hip(hipStreamWaitEvent(sh->s_post, pll, 0), "hipStreamWaitEvent");
+    check_hip(hipStreamWaitEvent(sh->s_post_c[indicator], pll, 0), "hipStreamWaitEvent");
 }
 
 // ------------------------------------------------------------------ audio (consumer 0)
@@ -355,7 +356,7 @@ void audio_thread(Shared* sh) {
     check_hip(hipSetDevice(o.device), "hipSetDevice");
     sdr_ctx* ctx = sh->ctx[1];
     const size_t n = 2 * (size_t)sh->info.n_audio, bytes = n * o.nch * sizeof(int16_t);
-    hipStream_t s = sh->s_post, sc = sh->s_d2h ? sh->s_d2h : sh->s_post;
+    hipStream_t s = sh->s_post_c[0], sc = sh->s_d2h ? sh->s_d2h : s;
     AudioRes& r = sh->ar;
     FILE* f = nullptr;
     if (o.out_prefix) {
@@ -411,7 +412,7 @@ void rds_thread(Shared* sh) {
     const sdr_multi_opts& o = sh->o;
     check_hip(hipSetDevice(o.device), "hipSetDevice");
     sdr_ctx* ctx = sh->ctx[2];
-    hipStream_t s = sh->s_post;
+    hipStream_t s = sh->s_post_c[1];
     RdsRes& r = sh->rr;
     hipEvent_t pre = r.pre, pll = r.pll, *out_ready = r.out_ready;   // [NH]
     int32_t *d_nbits = r.d_nbits, **h_nbits = r.h_nbits;
@@ -564,6 +565,8 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
     if (half > 0) {
         sh.s_fe = masked_stream(o.device, 0, o.pll_cus, 1);
         sh.s_post = masked_stream(o.device, 0, o.pll_cus, 1);
+        if (const char* e = std::getenv("SDR_MULTI_POSTS"); e && std::atoi(e) == 2)
+            sh.s_post_c[1] = masked_stream(o.device, 0, o.pll_cus, 1);
         sh.s_pll[0] = masked_stream(o.device, 0, half, 0);
         sh.s_pll[1] = masked_stream(o.device, half, half, 0);
         sh.persistent = sh.nblocks_known > 0;
@@ -580,6 +583,8 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
         sh.s_pll[0] = plain_stream();
         sh.s_pll[1] = plain_stream();
     }
+    sh.s_post_c[0] = sh.s_post;
+    if (!sh.s_post_c[1]) sh.s_post_c[1] = sh.s_post;
     if (o.in_path) sh.s_copy = plain_stream();
     // SDR_MULTI_D2H=copy: the L/R copies on a stream of their own instead of after the post stages
     if (const char* e = std::getenv("SDR_MULTI_D2H"); e && std::strcmp(e, "copy") == 0) sh.s_d2h = plain_stream();
@@ -641,6 +646,7 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
     free_consumers(&sh);
     for (sdr_ctx* c : sh.ctx) sdr_ctx_destroy(c);
     if (sh.s_d2h) (void)hipStreamDestroy(sh.s_d2h);
+    if (sh.s_post_c[1] != sh.s_post) (void)sdr_stream_destroy(sh.s_post_c[1]);
     for (hipStream_t s : {sh.s_fe, sh.s_post, sh.s_pll[0], sh.s_pll[1]}) {
         if (half > 0) (void)sdr_stream_destroy(s);
         else (void)hipStreamDestroy(s);
