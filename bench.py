@@ -1286,8 +1286,7 @@ def queue_plumbed_leg(args, st, nch: int) -> dict:
                  f"fresh contexts (the first, untimed like the bench's warm-up, gives the checked captures)",
         "value": round(q["blocks"] * samples / q["seconds"] / 1e6, 2), "unit": "MS/s",
         "ms_per_block": round(q["seconds"] / q["blocks"] * 1e3, 4),
-        "steady_value": (round((q["blocks"] - 1) * samples / q["steady_seconds"] / 1e6, 2)
-                         if q["steady_seconds"] else None),
+        "pll_period_value": (round(samples / (q["pll_period_ms"] * 1e-3) / 1e6, 2) if q["pll_period_ms"] else None),
         "pll_period_ms": round(q["pll_period_ms"], 4),
         "outside_pll_span_ms": round(q["seconds"] * 1e3 - q["pll_span_ms"], 3),
         "pll": "persistent" if q["persistent"] else "per-block dispatch",

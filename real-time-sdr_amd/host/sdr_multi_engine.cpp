@@ -207,12 +207,29 @@ struct Shared {
     sdr_ctx* ctx[3] = {};                // RF, audio, RDS (each thread owns its context)
     hipStream_t s_fe = nullptr, s_post = nullptr, s_pll[2] = {}, s_copy = nullptr;
     hipStream_t s_post_c[2] = {};        // consumer i's post stream: s_post, or its own (SDR_MULTI_POSTS=2)
+    // persistent mode: a stream over every CU for the first block's front-end side and the last
+    // block's post side (the PLL CUs idle then, as bench.py's fill and drain stream), and the events
+    // that order the switches (RF, audio, RDS)
+    hipStream_t s_all = nullptr;
+    hipEvent_t ev_first[3] = {}, ev_last[3] = {};
     bool persistent = false;
     long long nblocks_known = -1;        // -1: a byte stream of unknown length
     long long blocks = 0;
     double read_s = 0.0, h2d_ms = 0.0, d2h_ms = 0.0;   // input reads; GPU time of the H2D / L+R D2H copies
     std::chrono::steady_clock::time_point t_block1{};  // block 1's front end enqueued
 };
+
+// block b's front-end-side stream (the all-CU stream for the first block) and consumer i's post stream
+// (the all-CU stream for the last block)
+hipStream_t fe_stream(const Shared* sh, long long b) { return (sh->s_all && b == 0) ? sh->s_all : sh->s_fe; }
+hipStream_t post_stream(const Shared* sh, int i, long long b) {
+    return (sh->s_all && b == sh->nblocks_known - 1) ? sh->s_all : sh->s_post_c[i];
+}
+// work enqueued on `to` from now on follows the work enqueued on `from` so far
+void follow(hipStream_t to, hipStream_t from, hipEvent_t ev) {
+    check_hip(hipEventRecord(ev, from), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(to, ev, 0), "hipStreamWaitEvent");
+}
 
 // the host waits for a block's outputs by polling the event (yielding between polls) rather than
 // hipEventSynchronize, so a waiting consumer thread never sits inside the runtime while the other
@@ -300,12 +317,15 @@ void rf_thread(Shared* sh) {
             src = d_iq[k];
         }
         if (b == 1) sh->t_block1 = std::chrono::steady_clock::now();
-        check_sdr(sdr_frontend(ctx, src, stride, s), "sdr_frontend");
-        if (!dev_in) check_hip(hipEventRecord(fe_done[(int)(b & 1)], s), "hipEventRecord");
+        const hipStream_t sf = fe_stream(sh, b);
+        if (!dev_in && sf != s) check_hip(hipStreamWaitEvent(sf, h2d[(int)(b & 1)], 0), "hipStreamWaitEvent");
+        check_sdr(sdr_frontend(ctx, src, stride, sf), "sdr_frontend");
+        if (!dev_in) check_hip(hipEventRecord(fe_done[(int)(b & 1)], sf), "hipEventRecord");
         FmBatch* fb = sh->q.acquire();
-        for (auto& e : fb->released) check_hip(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
-        check_sdr(sdr_get_fm_demod(ctx, fb->d_fm, fb->stride, s), "sdr_get_fm_demod");
-        check_hip(hipEventRecord(fb->ready, s), "hipEventRecord");
+        for (auto& e : fb->released) check_hip(hipStreamWaitEvent(sf, e, 0), "hipStreamWaitEvent");
+        check_sdr(sdr_get_fm_demod(ctx, fb->d_fm, fb->stride, sf), "sdr_get_fm_demod");
+        check_hip(hipEventRecord(fb->ready, sf), "hipEventRecord");
+        if (sf != s) follow(s, sf, sh->ev_first[0]);       // block 1's front end after block 0's
         fb->block = b;
         sh->q.push(fb);                                     // rffrontend.cpp:74
         sh->blocks = b + 1;
@@ -326,7 +346,7 @@ bool consume(Shared* sh, sdr_ctx* ctx, int indicator) {
     FmBatch* fb = nullptr;
     sh->q.wait_and_pop(fb, indicator);
     if (!fb) return false;
-    hipStream_t s = sh->s_fe;
+    hipStream_t s = fe_stream(sh, fb->block);
     check_hip(hipStreamWaitEvent(s, fb->ready, 0), "hipStreamWaitEvent");
     check_sdr(sdr_push_fm_demod(ctx, fb->d_fm, fb->stride, s), "sdr_push_fm_demod");
     check_hip(hipEventRecord(fb->released[indicator], s), "hipEventRecord");
@@ -336,10 +356,13 @@ bool consume(Shared* sh, sdr_ctx* ctx, int indicator) {
 
 // the consumer's PLL of the block whose pre part is on s_fe: signal + wait on s_post (persistent),
 // or one dispatch on its own stream between two events
-void consumer_pll(Shared* sh, sdr_ctx* ctx, int indicator, hipEvent_t pre, hipEvent_t pll) {
+void consumer_pll(Shared* sh, sdr_ctx* ctx, int indicator, hipEvent_t pre, hipEvent_t pll, long long b) {
     if (sh->persistent) {
-        check_sdr(sdr_plls_signal(ctx, sh->s_fe), "sdr_plls_signal");
-        check_sdr(sdr_plls_wait(ctx, sh->s_post_c[indicator]), "sdr_plls_wait");
+        const hipStream_t sf = fe_stream(sh, b), sp = post_stream(sh, indicator, b);
+        check_sdr(sdr_plls_signal(ctx, sf), "sdr_plls_signal");
+        if (sf != sh->s_fe) follow(sh->s_fe, sf, sh->ev_first[1 + indicator]);   // block 1's pre after block 0's
+        if (sp != sh->s_post_c[indicator]) follow(sp, sh->s_post_c[indicator], sh->ev_last[1 + indicator]);
+        check_sdr(sdr_plls_wait(ctx, sp), "sdr_plls_wait");
         return;
     }
     check_hip(hipEventRecord(pre, sh->s_fe), "hipEventRecord");
@@ -356,7 +379,6 @@ void audio_thread(Shared* sh) {
     check_hip(hipSetDevice(o.device), "hipSetDevice");
     sdr_ctx* ctx = sh->ctx[1];
     const size_t n = 2 * (size_t)sh->info.n_audio, bytes = n * o.nch * sizeof(int16_t);
-    hipStream_t s = sh->s_post_c[0], sc = sh->s_d2h ? sh->s_d2h : s;
     AudioRes& r = sh->ar;
     FILE* f = nullptr;
     if (o.out_prefix) {
@@ -376,8 +398,9 @@ void audio_thread(Shared* sh) {
     };
     while (consume(sh, ctx, 0)) {
         const int k = (int)(b & 1), h = (int)(b % NH);
-        check_sdr(sdr_stereo_pre(ctx, sh->s_fe), "sdr_stereo_pre");
-        consumer_pll(sh, ctx, 0, r.pre, r.pll);
+        check_sdr(sdr_stereo_pre(ctx, fe_stream(sh, b)), "sdr_stereo_pre");
+        consumer_pll(sh, ctx, 0, r.pre, r.pll, b);
+        const hipStream_t s = post_stream(sh, 0, b), sc = sh->s_d2h ? sh->s_d2h : s;
         // d_lr[k] is free once block b-2's copy out of it is done (same stream, or the copy stream's event)
         if (sc != s && b >= 2) check_hip(hipStreamWaitEvent(s, r.out_ready[(b - 2) % NH], 0), "hipStreamWaitEvent");
         check_sdr(sdr_stereo_post(ctx, r.d_lr[k], n, s), "sdr_stereo_post");
@@ -394,7 +417,8 @@ void audio_thread(Shared* sh) {
     }
     for (long long blk = std::max(0LL, b - LAG); blk < b; blk++) write_block(blk);
     if (f) std::fclose(f);
-    check_hip(hipStreamSynchronize(sc), "hipStreamSynchronize");
+    for (hipStream_t x : {sh->s_post_c[0], sh->s_d2h, sh->s_all})
+        if (x) check_hip(hipStreamSynchronize(x), "hipStreamSynchronize");
 }
 
 // ------------------------------------------------------------------ RDS (consumer 1)
@@ -412,7 +436,6 @@ void rds_thread(Shared* sh) {
     const sdr_multi_opts& o = sh->o;
     check_hip(hipSetDevice(o.device), "hipSetDevice");
     sdr_ctx* ctx = sh->ctx[2];
-    hipStream_t s = sh->s_post_c[1];
     RdsRes& r = sh->rr;
     hipEvent_t pre = r.pre, pll = r.pll, *out_ready = r.out_ready;   // [NH]
     int32_t *d_nbits = r.d_nbits, **h_nbits = r.h_nbits;
@@ -452,8 +475,9 @@ void rds_thread(Shared* sh) {
     long long b = 0;
     while (consume(sh, ctx, 1)) {
         const int k = (int)(b % NH);
-        check_sdr(sdr_rds_pre(ctx, sh->s_fe), "sdr_rds_pre");
-        consumer_pll(sh, ctx, 1, pre, pll);
+        check_sdr(sdr_rds_pre(ctx, fe_stream(sh, b)), "sdr_rds_pre");
+        consumer_pll(sh, ctx, 1, pre, pll, b);
+        const hipStream_t s = post_stream(sh, 1, b);
         check_sdr(sdr_rds_post(ctx, nullptr, 0, s), "sdr_rds_post");
         check_sdr(sdr_rds_bits(ctx, nullptr, nullptr, nullptr, 0, d_nbits, d_bits, SDR_MAX_BITS, s), "sdr_rds_bits");
         check_hip(hipMemcpyAsync(h_nbits[k], d_nbits, o.nch * sizeof(int32_t), hipMemcpyDeviceToHost, s),
@@ -474,7 +498,8 @@ void rds_thread(Shared* sh) {
         }
         std::fclose(f);
     }
-    check_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+    for (hipStream_t x : {sh->s_post_c[1], sh->s_all})
+        if (x) check_hip(hipStreamSynchronize(x), "hipStreamSynchronize");
 }
 
 void alloc_consumers(Shared* sh) {
@@ -577,6 +602,18 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
                                     &groups, &resident), "sdr_plls_fits");
             sh.persistent = groups <= resident;
         }
+        if (sh.persistent) {   // the fill and drain stream (SDR_MULTI_EDGES=0: none)
+            const char* ed = std::getenv("SDR_MULTI_EDGES");
+            if (!ed || std::atoi(ed) != 0) {
+                hipDeviceProp_t prop;
+                check_hip(hipGetDeviceProperties(&prop, o.device), "hipGetDeviceProperties");
+                sh.s_all = masked_stream(o.device, 0, prop.multiProcessorCount, 0);
+                for (int i = 0; i < 3; i++) {
+                    sh.ev_first[i] = new_event();
+                    sh.ev_last[i] = new_event();
+                }
+            }
+        }
     } else {
         sh.s_fe = plain_stream();
         sh.s_post = plain_stream();
@@ -647,6 +684,10 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
     for (sdr_ctx* c : sh.ctx) sdr_ctx_destroy(c);
     if (sh.s_d2h) (void)hipStreamDestroy(sh.s_d2h);
     if (sh.s_post_c[1] != sh.s_post) (void)sdr_stream_destroy(sh.s_post_c[1]);
+    if (sh.s_all) (void)sdr_stream_destroy(sh.s_all);
+    for (int i = 0; i < 3; i++)
+        for (hipEvent_t ev : {sh.ev_first[i], sh.ev_last[i]})
+            if (ev) (void)hipEventDestroy(ev);
     for (hipStream_t s : {sh.s_fe, sh.s_post, sh.s_pll[0], sh.s_pll[1]}) {
         if (half > 0) (void)sdr_stream_destroy(s);
         else (void)hipStreamDestroy(s);
