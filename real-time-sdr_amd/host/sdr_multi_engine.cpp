@@ -212,6 +212,19 @@ struct Shared {
     // that order the switches (RF, audio, RDS)
     hipStream_t s_all = nullptr;
     hipEvent_t ev_first[3] = {}, ev_last[3] = {};
+    // the threads start before the clock: each makes its first runtime calls (per-thread HIP state),
+    // reports ready and waits for the go
+    std::mutex start_mu;
+    std::condition_variable start_cv;
+    int ready = 0;
+    bool go = false;
+    void arrive_and_wait() {
+        (void)hipStreamQuery(s_fe);
+        std::unique_lock<std::mutex> lk(start_mu);
+        ready++;
+        start_cv.notify_all();
+        start_cv.wait(lk, [this] { return go; });
+    }
     bool persistent = false;
     long long nblocks_known = -1;        // -1: a byte stream of unknown length
     long long blocks = 0;
@@ -264,6 +277,7 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b) {
 void rf_thread(Shared* sh) {
     const sdr_multi_opts& o = sh->o;
     check_hip(hipSetDevice(o.device), "hipSetDevice");
+    sh->arrive_and_wait();
     sdr_ctx* ctx = sh->ctx[0];
     const sdr_info& in = sh->info;
     const size_t row = 2 * (size_t)in.block_iq, bytes = row * o.nch;
@@ -377,6 +391,7 @@ void consumer_pll(Shared* sh, sdr_ctx* ctx, int indicator, hipEvent_t pre, hipEv
 void audio_thread(Shared* sh) {
     const sdr_multi_opts& o = sh->o;
     check_hip(hipSetDevice(o.device), "hipSetDevice");
+    sh->arrive_and_wait();
     sdr_ctx* ctx = sh->ctx[1];
     const size_t n = 2 * (size_t)sh->info.n_audio, bytes = n * o.nch * sizeof(int16_t);
     AudioRes& r = sh->ar;
@@ -435,6 +450,7 @@ struct FrameState {   // rds.cpp:67-92, per channel
 void rds_thread(Shared* sh) {
     const sdr_multi_opts& o = sh->o;
     check_hip(hipSetDevice(o.device), "hipSetDevice");
+    sh->arrive_and_wait();
     sdr_ctx* ctx = sh->ctx[2];
     RdsRes& r = sh->rr;
     hipEvent_t pre = r.pre, pll = r.pll, *out_ready = r.out_ready;   // [NH]
@@ -648,10 +664,17 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
         check_sdr(sdr_plls_launch_sel(sh.ctx[2], (int)sh.nblocks_known, SDR_PLLS_RDS, sh.s_pll[1]), "sdr_plls_launch_sel");
     }
     if (const char* e = std::getenv("SDR_MULTI_SYNC"); e && std::strcmp(e, "event") == 0) g_poll_events = false;
-    const auto t0 = std::chrono::steady_clock::now();
     std::thread t_rds(rds_thread, &sh);      // project.cpp:134-136
     std::thread t_audio(audio_thread, &sh);
     std::thread t_rf(rf_thread, &sh);
+    std::chrono::steady_clock::time_point t0;
+    {
+        std::unique_lock<std::mutex> lk(sh.start_mu);
+        sh.start_cv.wait(lk, [&sh] { return sh.ready == 3; });
+        t0 = std::chrono::steady_clock::now();
+        sh.go = true;
+        sh.start_cv.notify_all();
+    }
     t_rf.join();
     t_audio.join();
     t_rds.join();
