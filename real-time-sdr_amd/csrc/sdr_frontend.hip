@@ -120,6 +120,12 @@ constexpr int FE_PF = 5;           // tap rows prefetched this many samples ahea
 // exact front end: outputs per lane (16 halves the occupancy: 1.54x slower, profiles/r04/ab_fe_r16.txt;
 // 12 or 16 with the next tile's window prefetched in registers: slower too, profiles/r04/ab_fe_v4.txt)
 constexpr int FE_R = 8;
+// exact discriminator: 1 = reciprocal + Newton step with a tie proof (IEEE division as the fallback),
+// 0 = the IEEE f64 division on every output
+#ifndef SDR_FE_DISC
+#define SDR_FE_DISC 1
+#endif
+constexpr uint32_t FE_TIE_ULPS = 2048;   // > the fast quotient's 550-ulp error bound, with margin
 // {h, h} * m with h one half (HI) of an SGPR pair: v_pk_mul_f32 with a scalar operand whose half
 // is broadcast to both lanes by op_sel / op_sel_hi (no VGPR copy of the tap)
 __device__ __forceinline__ f32x2 fe_mul_v(double hpair, int hi, f32x2 m) {
@@ -496,29 +502,77 @@ __global__ __launch_bounds__(64) void k_frontend2(
     const f32x2 left = f32x2{__shfl_up(acc[R - 1].x, 1), __shfl_up(acc[R - 1].y, 1)};
     float* out = fm + (size_t)ch * fm_stride;
     const int cbase = c0 + t * R;
+    float v[R];
+#if SDR_FE_DIAG & 2
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int c = cbase + r;
+    for (int r = 0; r < R; r++) v[r] = acc[r].x + ((r > 0) ? acc[r > 0 ? r - 1 : 0] : left).y;
+#else
+    // the previous sample of output r; output 0 of the block (its previous sample is the last block's
+    // carry, prev_in) can only be output 1 of lane 0 of tile 0 (c0 = j*ADV - 1 >= -1)
+    auto prev = [&](int r) -> f32x2 {
         f32x2 pv = (r > 0) ? acc[r > 0 ? r - 1 : 0] : left;
-        if (c == 0) {
+        if (r == 1 && cbase == -1) {
             const float2 p = prev_in[ch];
             pv = f32x2{p.x, p.y};
         }
-        const f32x2 cur = acc[r];
-        float v;
-#if SDR_FE_DIAG & 2
-        v = cur.x + pv.y;
+        return pv;
+    };
+#if SDR_FE_DISC
+    // The reference's value is RN32(RN64(num / den)), den = RN64(I^2 + Q^2) (pow(x, 2.0) is exact
+    // in f64, so den is one fma). Instead of the IEEE f64 division: q = RN64(num * r1), r1 = 1/den
+    // from v_rcp_f64 (~2^-23 relative) refined by one Newton step, so |q / (num/den) - 1| < 2^-43.9,
+    // i.e. < 550 ulps of q. RN32(q) equals the reference's value unless q lies within FE_TIE_ULPS
+    // ulps of an f32 rounding tie (the tie key) or rounds to an f32 subnormal: a lane with any such
+    // output recomputes its outputs by the division (a branch taken by ~1e-5 of the lanes).
+    uint32_t kmin = 0xFFFFFFFFu;
+    bool sub = false;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const f32x2 cur = acc[r], pv = prev(r);
+        const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
+        const double dI = (double)cur.x, dQ = (double)cur.y;
+        const double den = __builtin_fma(dI, dI, dQ * dQ);
+        const double r0 = __builtin_amdgcn_rcp(den);
+        const double r1 = __builtin_fma(r0, __builtin_fma(-den, r0, 1.0), r0);
+        const double q = (double)num * r1;
+        const float vq = (float)q;
+        const uint32_t key = ((uint32_t)__builtin_bit_cast(uint64_t, q) << 3) + (0x80000000u + 8u * FE_TIE_ULPS);
+        kmin = key < kmin ? key : kmin;
+        sub |= __builtin_amdgcn_classf(vq, 0x90);   // negative or positive f32 subnormal
+        v[r] = den == 0.0 ? 0.0f : vq;              // (I, Q) = (0, 0): demod.cpp:15-16
+    }
+    if (kmin <= 16u * FE_TIE_ULPS || sub) {
 #else
-        if ((cur.x == 0) & (cur.y == 0)) {
-            v = 0.0f;
-        } else {
-            const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
-            const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
-            v = (float)((double)num / den);
-        }
+    {
 #endif
-        if (c > c0 && c >= 0 && c < block_if) out[c] = v;
-        if (c == block_if - 1) prev_out[ch] = make_float2(cur.x, cur.y);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const f32x2 cur = acc[r], pv = prev(r);
+            if ((cur.x == 0) & (cur.y == 0)) {
+                v[r] = 0.0f;
+            } else {
+                const float num = cur.x * (cur.y - pv.y) - cur.y * (cur.x - pv.x);
+                const double den = (double)cur.x * (double)cur.x + (double)cur.y * (double)cur.y;
+                v[r] = (float)((double)num / den);
+            }
+        }
+    }
+#endif
+    if (t > 0 && cbase + R < block_if) {             // all R outputs written, none the block's last
+        if ((reinterpret_cast<uintptr_t>(out + cbase) & 7) == 0) {
+#pragma unroll
+            for (int r = 0; r < R; r += 2) *reinterpret_cast<float2*>(out + cbase + r) = make_float2(v[r], v[r + 1]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; r++) out[cbase + r] = v[r];
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int c = cbase + r;
+            if (c > c0 && c >= 0 && c < block_if) out[c] = v[r];
+            if (c == block_if - 1) prev_out[ch] = make_float2(acc[r].x, acc[r].y);
+        }
     }
     if (j == 0) {
         const uint16_t* last = reinterpret_cast<const uint16_t*>(src) + (block_iq - HP);

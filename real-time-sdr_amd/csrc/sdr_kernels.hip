@@ -1777,6 +1777,20 @@ extern "C" int sdr_diag_hold(void* stream, int ms) {
     return SDR_OK;
 }
 
+// Test support (not part of sdr_amd.h): res[i] = 1 - x[i] * v_rcp_f64(x[i]) (one fma, exact), the
+// hardware reciprocal's relative error that the exact front end's discriminator proof assumes
+// below 2^-22 (sdr_frontend.hip, SDR_FE_DISC; tests/test_gpu_primitives.py).
+__global__ void k_rcp64_residual(const double* __restrict__ x, double* __restrict__ res, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) res[i] = __builtin_fma(-x[i], __builtin_amdgcn_rcp(x[i]), 1.0);
+}
+extern "C" int sdr_diag_rcp64_residual(const double* x, double* res, int n, void* stream) {
+    if (!x || !res || n <= 0) return fail(SDR_E_INVALID, "sdr_diag_rcp64_residual: bad arguments");
+    hipLaunchKernelGGL(k_rcp64_residual, dim3((n + 255) / 256), dim3(256), 0, S(stream), x, res, n);
+    HIP_TRY(hipGetLastError());
+    return SDR_OK;
+}
+
 // Diagnosis builds only (-DSDR_PLL_COUNT=1): the PLL chunk counters; -1 in product builds.
 // Not part of sdr_amd.h.
 extern "C" int sdr_diag_pll_counts(unsigned long long* out, int reset) { return diag_pll_counts(out, reset); }

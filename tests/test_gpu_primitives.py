@@ -81,6 +81,30 @@ def test_fm_demod(pkg, oracle, torch_cuda):
             assert np.array_equal(d_prev[c].cpu().numpy(), prev_ref[c])
 
 
+def test_rcp64_error_within_discriminator_bound(pkg, torch_cuda):
+    """The exact front end's discriminator (sdr_frontend.hip, SDR_FE_DISC) takes RN32(num * r1) with
+    r1 = v_rcp_f64(den) + one Newton step as the reference's RN32(RN64(num / den)) (demod.cpp:11-18)
+    when no f32 tie lies within 2048 ulps; its bound needs the hardware reciprocal within 2^-22
+    relative. Every one of the 2^24 leading-mantissa patterns (random low bits, exponents over the
+    discriminator's range of I^2 + Q^2), through the library's residual kernel."""
+    import ctypes as C
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    n = 1 << 24
+    mant = (np.arange(n, dtype=np.uint64) << np.uint64(28)) | rng.integers(0, 1 << 28, n, dtype=np.uint64)
+    expo = rng.integers(1023 - 200, 1023 + 40, n, dtype=np.uint64)
+    x = torch.from_numpy((mant | (expo << np.uint64(52))).view(np.float64)).cuda()
+    res = torch.empty_like(x)
+    L = pkg.lib()
+    L.sdr_diag_rcp64_residual.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.sdr_diag_rcp64_residual.restype = C.c_int
+    pkg.check(L.sdr_diag_rcp64_residual(C.c_void_p(x.data_ptr()), C.c_void_p(res.data_ptr()), n,
+                                        C.c_void_p(torch.cuda.current_stream().cuda_stream)), "rcp64")
+    worst = float(res.abs().max().item())
+    print(f"v_rcp_f64 max relative error 2^{np.log2(worst):.2f}")
+    assert worst < 2.0 ** -22
+
+
 @pytest.mark.parametrize("freq,nco,bw", [(19e3, 2.0, 0.01), (114e3, 0.5, 0.001)])
 def test_fmpll(pkg, oracle, torch_cuda, freq, nco, bw):
     torch = torch_cuda
