@@ -38,9 +38,6 @@ host: $(HOSTLIB) $(CLI) $(MULTI)
 # profiles/r03/ab_pll_split3.txt)
 build/sdr_kernels.hip.o: HIPFLAGS += -fno-slp-vectorize
 build/sdr_pll.hip.o: HIPFLAGS += -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp
-# the prefetching front end takes tiles with a one-lane atomic whose result is read half a tile later:
-# no wave-level atomic rewrite (it reads the result right after the atomic)
-build/sdr_frontend.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 # (the lane-pair PLL step scheduled for ILP: 212.4 -> 210.4 shader cycles per step, profiles/r04/ab_sched.txt)
 
 build/%.o: $(PKG)/csrc/% $(HDRS) Makefile

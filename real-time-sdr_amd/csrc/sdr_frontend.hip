@@ -346,29 +346,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     }
 }
 
-// The FIR sweep of one tile: lane t's R outputs from its TWIN-sample window at sw + 2 t R D.
-// PF = false: the window holds sign-flipped bytes; chunks are read from LDS two ahead of their use.
-// PF = true (k_frontend_pf): raw u8 from LDS-DMA, flipped as they are converted; the upper half of
-// the lane's window is read first and the lower half at mid-sweep, after which `mid` runs (the LDS
-// buffer is free: k_frontend_pf issues the next tile's DMA there).
-template <int R, int D, bool PF, class Mid>
-__device__ __forceinline__ void fe_fir(const uint8_t* __restrict__ sw, const float* __restrict__ hs, f32x2 (&acc)[R],
-                                       Mid&& mid) {
+// The FIR sweep of one tile: lane t's R outputs from its TWIN-sample window of sign-flipped bytes at
+// sw + 2 t R D; 16-byte chunks are read from LDS two ahead of their use.
+template <int R, int D>
+__device__ __forceinline__ void fe_fir(const uint8_t* __restrict__ sw, const float* __restrict__ hs, f32x2 (&acc)[R]) {
     constexpr int NT = 101, HP = NT - 1;
     constexpr int TWIN = (R - 1) * D + NT;            // samples one thread reads
     constexpr int TCH = (2 * TWIN + 15) / 16;         // 16-byte LDS chunks per thread window
-    constexpr int H = TCH / 2;                        // PF: chunks [H, TCH) first, [0, H) at mid-sweep
-    static_assert(!PF || (H >= 1 && 8 * (H + 1) + 7 <= TWIN - 1), "PF: mid() runs exactly once");
     const int t = threadIdx.x;
     uint4 chunk[TCH];
     const uint4* tw = reinterpret_cast<const uint4*>(sw + 2 * t * R * D);
-    if (PF) {
-#pragma unroll
-        for (int c = H; c < TCH; c++) chunk[c] = tw[c];
-    } else {
-        chunk[TCH - 1] = tw[TCH - 1];
-        if (TCH >= 2) chunk[TCH - 2] = tw[TCH - 2];
-    }
+    chunk[TCH - 1] = tw[TCH - 1];
+    if (TCH >= 2) chunk[TCH - 2] = tw[TCH - 2];
 #pragma unroll
     for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
     // Taps live in SGPRs: row S of the table holds the R taps sample S meets (uniform across the
@@ -392,8 +381,7 @@ __device__ __forceinline__ void fe_fir(const uint8_t* __restrict__ sw, const flo
     auto sample = [&](int S) -> f32x2 {
         const uint4 c4 = chunk[S >> 3];
         const int dw = (S & 7) >> 1;
-        uint32_t w = dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w;   // signed bytes (staging)
-        if (PF) w ^= 0x80808080u;                      // raw u8 (LDS-DMA): u ^ 0x80 = u - 128 as int8
+        const uint32_t w = dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w;   // signed bytes (staging)
 #if SDR_FE_DIAG & 1
         return f32x2{__builtin_bit_cast(float, w & 0x3F3F3F3Fu), __builtin_bit_cast(float, w & 0x3E3E3E3Eu)};
 #else
@@ -405,15 +393,7 @@ __device__ __forceinline__ void fe_fir(const uint8_t* __restrict__ sw, const flo
 #pragma unroll
     for (int S = TWIN - 1; S >= 0; S--) {
         const int slot = S % FE_PF;
-        if (PF) {
-            if ((S & 7) == 7 && (S >> 3) == H + 1) {   // the lower half, two chunks before its first use
-#pragma unroll
-                for (int c = 0; c < H; c++) chunk[c] = tw[c];
-            }
-            if ((S & 7) == 7 && (S >> 3) == H - 1) mid();   // every LDS read of the window issued
-        } else if (((S & 7) == 7 || S == TWIN - 1) && (S >> 3) >= 2) {
-            chunk[(S >> 3) - 2] = tw[(S >> 3) - 2];
-        }
+        if (((S & 7) == 7 || S == TWIN - 1) && (S >> 3) >= 2) chunk[(S >> 3) - 2] = tw[(S >> 3) - 2];
         const f32x2 m = m_next;
         // all products of the sample first, then the adds, in program order (volatile asm): no add
         // waits on the product issued just before it (filter.cpp:115: multiply, then add)
@@ -609,7 +589,7 @@ __global__ __launch_bounds__(64) void k_frontend2(
     }
     __syncthreads();
     f32x2 acc[R];
-    fe_fir<R, D, false>(sw, hs, acc, [] {});
+    fe_fir<R, D>(sw, hs, acc);
     fe_disc_store<R>(acc, c0, ch, prev_in, prev_out, fm + (size_t)ch * fm_stride, block_if);
     float* out = fm + (size_t)ch * fm_stride;
     if (j == 0) {
@@ -622,92 +602,6 @@ __global__ __launch_bounds__(64) void k_frontend2(
     if (stamps) {   // the end: after this wave's stores have completed
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (threadIdx.x == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-}
-
-// Exact front end, persistent, the window prefetched by LDS-DMA: the same tiles, FIR and
-// discriminator as k_frontend2, but each wave runs tiles blockIdx.x, + gridDim.x, ... (a grid the
-// stream's CUs hold at once, 15 waves per CU by the LDS buffer) and never waits for a window:
-// tile i's u8 window reaches the wave's LDS buffer by global_load_lds_dword (raw bytes, 256
-// coalesced bytes per instruction; boundary tiles point single lanes at the tail or the padding),
-// each lane reads its window into registers in two halves, and once the lower half is read the next
-// tile's DMA goes into the same buffer, so its HBM latency hides behind the rest of the sweep. The
-// sign flip moves to the conversion. Rows must be dword aligned (frontend_args). Stamps per tile, as
-// k_frontend2's per workgroup. (Tiles taken from one device counter instead: 2.6x slower, every
-// wave's atomic on one address serialises, profiles/r06/frontend_pf/.)
-template <int R, int D>
-__global__ __launch_bounds__(64) void k_frontend_pf(
-    const uint8_t* __restrict__ iq, size_t iq_stride, const uint8_t* __restrict__ tail_in,
-    uint8_t* __restrict__ tail_out, const float2* __restrict__ prev_in, float2* __restrict__ prev_out,
-    const float* __restrict__ hs, int block_iq, int block_if,
-    float* __restrict__ fm, const float* __restrict__ fm_other, size_t fm_stride, int j0, int jn,
-    const uint32_t* __restrict__ pad, unsigned long long* __restrict__ stamps, int ntiles) {
-    static_assert(D % 2 == 0, "whole dwords of I/Q pairs");
-    constexpr int NT = 101, HP = NT - 1, NTH = 64;
-    constexpr int TILE = NTH * R, ADV = TILE - 1, WIN = (TILE - 1) * D + NT;
-    constexpr int TWIN = (R - 1) * D + NT, TCH = (2 * TWIN + 15) / 16;
-    constexpr int NG = (2 * WIN + 3) / 4, PER = (NG + NTH - 1) / NTH;
-    static_assert(2 * (NTH - 1) * R * D + 16 * TCH <= PER * 256, "every lane window inside the DMA buffer");
-    __shared__ __attribute__((aligned(16))) uint8_t sw[PER * 256];
-    const int t = threadIdx.x;
-    // tile tl's window into sw: dword i (lane i % 64 of instruction i / 64) from the block, the
-    // previous block's tail or the padding (u8 128 = 0.0f), as k_frontend2's staging
-    auto issue = [&](int tl) {
-#if SDR_FE_DIAG & 8
-        tl = 1;   // diagnosis: every DMA fetches channel 0's tile 1 (an L2-resident window)
-#endif
-        const int ch = tl / jn, j = j0 + tl - ch * jn;
-        const int m0 = (j * ADV - 1) * D - HP;
-        const uint8_t* src = iq + (size_t)ch * iq_stride;
-        const uint8_t* tin = tail_in + (size_t)ch * 2 * HP;
-        const uint8_t* pd = reinterpret_cast<const uint8_t*>(pad);
-        if (m0 >= 0 && m0 + WIN <= block_iq) {        // interior: one base address, immediate offsets
-            const uint8_t* a0 = src + 2 * m0 + 4 * t;
-#pragma unroll
-            for (int k = 0; k < PER - 1; k++)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(a0 + 256 * k), sw + 256 * k, 4, 0, 0);
-            const uint8_t* al = (t + NTH * (PER - 1) < NG) ? a0 + 256 * (PER - 1) : pd;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(al), sw + 256 * (PER - 1), 4, 0, 0);
-        } else {
-            for (int k = 0; k < PER; k++) {
-                const int i = t + NTH * k;
-                const int mm = m0 + 2 * i;
-                const uint8_t* a = (i >= NG) ? pd : mm >= 0 ? (mm < block_iq ? src + 2 * mm : pd)
-                                                             : (mm >= -HP ? tin + 2 * (HP + mm) : pd);
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(a), sw + 256 * k, 4, 0, 0);
-            }
-        }
-    };
-    int tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    issue(tile);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (;;) {
-        if (stamps && t == 0) stamps[2 * tile] = __builtin_amdgcn_s_memrealtime();
-        const int nxt = tile + (int)gridDim.x;
-        const int ch = tile / jn, j = j0 + tile - ch * jn;
-        const int c0 = j * ADV - 1;
-        f32x2 acc[R];
-        fe_fir<R, D, true>(sw, hs, acc, [&] {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every lane has read its window
-            if (nxt < ntiles) issue(nxt);
-        });
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // the next window has landed
-        float* out = fm + (size_t)ch * fm_stride;
-        fe_disc_store<R>(acc, c0, ch, prev_in, prev_out, out, block_if);
-        if (j == 0) {
-            const uint16_t* last = reinterpret_cast<const uint16_t*>(iq + (size_t)ch * iq_stride) + (block_iq - HP);
-            uint16_t* tout = reinterpret_cast<uint16_t*>(tail_out + (size_t)ch * 2 * HP);
-            for (int i = t; i < HP; i += NTH) tout[i] = last[i];
-            const float* o = fm_other + (size_t)ch * fm_stride;
-            for (int i = t; i < HIST; i += NTH) out[i - HIST] = o[block_if - HIST + i];
-        }
-        if (stamps) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (t == 0) stamps[2 * tile + 1] = __builtin_amdgcn_s_memrealtime();
-        }
-        if (nxt >= ntiles) break;
-        tile = nxt;
     }
 }
 
@@ -761,24 +655,6 @@ int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0, int jn) {
         else if (a.D == 4) { if (x4) FEM(4, true); else FEM(4, false); }
         else { if (x4) FEM(3, true); else FEM(3, false); }
 #undef FEM
-    } else if (a.ntaps == 101 && a.pf && (a.D == 10 || a.D == 4)) {
-        // persistent waves, as many as the stream's CUs hold (15 per CU: the LDS buffer), each with the
-        // same number of tiles
-        const int ntiles = jn * a.nch;
-        static const int wpc = [] {
-            const char* e = std::getenv("SDR_FE_PF_WPC");   // A/B only: waves per CU of the grid
-            const int v = e ? std::atoi(e) : 15;
-            return v >= 1 && v <= 15 ? v : 15;
-        }();
-        const int per_wave = cdiv(ntiles, std::max(a.cus, 1) * wpc);
-        const int grid = cdiv(ntiles, per_wave);
-#define FEP(DD)                                                                                               \
-        hipExtLaunchKernelGGL((k_frontend_pf<FE_R, DD>), dim3(grid), dim3(64), 0, s, a.ev0, a.ev1, 0, iq, iq_stride,  \
-                              tail_in, tail_out, prev_in, prev_out, a.hs, a.block_iq, a.block_if, fm_p, fm_o,         \
-                              a.fm_stride, j0, jn, a.pad80, a.stamps, ntiles)
-        if (a.D == 10) FEP(10);
-        else FEP(4);
-#undef FEP
     } else if (a.ntaps == 101 && a.D == 10) {
         FE2(10);
     } else if (a.ntaps == 101 && a.D == 4) {

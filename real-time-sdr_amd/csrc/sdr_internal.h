@@ -19,11 +19,6 @@
 #include "sdr_amd.h"
 
 #define SDRK_HIDDEN __attribute__((visibility("hidden")))
-// the exact front end's form unless SDR_FE_PF is set: 0 = k_frontend2 (one tile per workgroup),
-// 1 = k_frontend_pf (persistent waves, next window by LDS-DMA)
-#ifndef SDR_FE_PF_DEFAULT
-#define SDR_FE_PF_DEFAULT 0
-#endif
 
 namespace sdrk SDRK_HIDDEN {
 
@@ -110,10 +105,6 @@ struct FrontendArgs {
     bool fast;
     hipEvent_t ev0, ev1;       // non-null: HIP events recorded with the launch (sdr_frontend_timing)
     unsigned long long* stamps;   // non-null (k_frontend2): [workgroup][start, end] on the 100 MHz clock
-    // k_frontend_pf (exact front end, persistent, LDS-DMA prefetch): used when pf, with a grid sized
-    // for cus CUs (the launch stream's)
-    bool pf;
-    int cus;
 };
 // the whole block (jn <= 0) or tiles [j0, j0 + jn) of every channel (exact front end only)
 int frontend_launch(const FrontendArgs& a, hipStream_t s, int j0 = 0, int jn = 0);
@@ -217,7 +208,6 @@ struct sdr_ctx {
     sdr_pll_state *st_pll = nullptr, *rds_pll = nullptr;
     int32_t* dec = nullptr;                             // [nch][DEC_STATE]
     uint32_t* pad80 = nullptr;                          // 64 words of u8 128 (the zero sample)
-    bool fe_pf = false;                                 // exact front end: k_frontend_pf (SDR_FE_PF)
     void* fe_afrag = nullptr;                           // MFMA front end: tap digit fragments
     double fe_yscale = 0.0;                             // 2^-(F+7): fixed-point taps, x = (u-128)/128
     int cus = 0;                                        // compute units of the device

@@ -1644,13 +1644,6 @@ bool masked_stream(hipStream_t s, int* device, CuPlacement* place) {
     return false;
 }
 
-// the CUs a stream's kernels run on: its mask's (sdr_stream_create_cu_range) or the device's
-int stream_cus(const sdr_ctx* c, hipStream_t s) {
-    int dev = 0;
-    CuPlacement pl{};
-    return masked_stream(s, &dev, &pl) ? pl.ncu : c->cus;
-}
-
 // the mask of CUs [first_cu, first_cu + n_cu) of a device (or of every other CU: exclude)
 std::vector<uint32_t> cu_range_mask(int ncu, int first_cu, int n_cu, int exclude, int* nset) {
     std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
@@ -1823,10 +1816,6 @@ int sdr_ctx_create(sdr_ctx** out, int device, int nch, int mode, int rds_on, int
         int cus = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         c->cus = cus;
-    }
-    {
-        const char* pf = std::getenv("SDR_FE_PF");   // the exact front end's persistent prefetching form
-        c->fe_pf = pf ? std::atoi(pf) != 0 : SDR_FE_PF_DEFAULT;
     }
     int r = fill_info(&c->info, nch, mode, c->rds_on);
     if (r) { delete c; return r; }
@@ -2045,9 +2034,6 @@ FrontendArgs frontend_args(const sdr_ctx* c, const uint8_t* iq, size_t iq_stride
     a.yscale = c->fe_yscale;
     a.pad80 = c->pad80;
     a.fast = (c->flags & SDR_FLAG_FAST_FRONTEND) != 0 && c->fe_afrag != nullptr;
-    // the prefetching front end's DMA reads whole dwords of each row
-    a.pf = c->fe_pf && !a.fast && (reinterpret_cast<uintptr_t>(iq) & 3) == 0 && (iq_stride & 3) == 0;
-    a.cus = c->cus;
     return a;
 }
 // Parity release across streams (threadsafequeue.h:29-31: a producer reuses a buffer only after its
@@ -2143,7 +2129,6 @@ int sdr_frontend(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, void* stream) 
         a.ev0 = c->fe_ev[2 * c->fe_time_n];
         a.ev1 = c->fe_ev[2 * c->fe_time_n + 1];
     }
-    a.cus = stream_cus(c, S(stream));
     const int r = frontend_launch(a, S(stream));
     if (r) return r;
     if (timed) c->fe_time_n++;
@@ -2758,8 +2743,7 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
     const int n = c->info.block_if, ntiles = cdiv(n, FRB_TILE), fe_tiles = frontend_tiles(n);
     nparts = std::min(nparts, ntiles);
     const int p = c->parity ^ 1;
-    FrontendArgs a = frontend_args(c, iq, iq_stride, p);
-    a.cus = stream_cus(c, s);
+    const FrontendArgs a = frontend_args(c, iq, iq_stride, p);
     if (const int rw = release_wait(c, p, REL_MONO | REL_STEREO | REL_RDS, s)) return rw;
     const int parity0 = c->parity;
     const long long block0 = c->block;

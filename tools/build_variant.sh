@@ -13,7 +13,7 @@ for f in sdr_kernels.hip sdr_frontend.hip sdr_pll.hip sdr_taps.cpp; do
   extra=""
   case $f in
     sdr_kernels.hip) extra="-fno-slp-vectorize ${KFLAGS:-}";;
-    sdr_frontend.hip) extra="-mllvm -amdgpu-atomic-optimizer-strategy=None ${FEFLAGS:-}";;
+    sdr_frontend.hip) extra="${FEFLAGS:-}";;
     sdr_pll.hip) extra="-fno-slp-vectorize ${PLLFLAGS--mllvm -amdgpu-sched-strategy=max-ilp}";;
   esac
   /opt/rocm/bin/hipcc $common $extra "$@" -c -o $d/$f.o real-time-sdr_amd/csrc/$f & pids="$pids $!"
