@@ -59,8 +59,11 @@ typedef struct sdr_multi_stats {
     int persistent;               /* 1: persistent PLL launches, 0: per-block dispatches */
 } sdr_multi_stats;
 
-/* Runs the receiver to the end of the input. 0 on success; otherwise an sdr_amd.h error code with
- * the text in sdr_last_error() (or, for I/O and HIP runtime failures, SDR_E_HIP / SDR_E_INVALID). */
+/* Runs the receiver to the end of the input and returns 0; SDR_E_INVALID for invalid options (nothing
+ * started). Once its threads run, a failure -- an unreadable input or output file, a library or HIP
+ * runtime error, a persistent PLL launch that timed out -- prints "sdr: <what>" on stderr and ends the
+ * process with exit(1), as the reference program does (rffrontend.cpp:50-52, utilities.h:7-10): the
+ * three stage threads cannot be unwound from each other's queue waits. */
 int sdr_multi_run(const sdr_multi_opts *opts, sdr_multi_stats *stats);
 
 #ifdef __cplusplus
