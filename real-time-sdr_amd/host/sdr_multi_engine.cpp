@@ -599,7 +599,10 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
     check_sdr(sdr_ctx_create(&sh.ctx[2], o.device, o.nch, o.mode, 1, o.flags), "sdr_ctx_create");
     check_sdr(sdr_ctx_info(sh.ctx[0], &sh.info), "sdr_ctx_info");
     const size_t row = 2 * (size_t)sh.info.block_iq;
-    if (!o.in_path && o.row_stride < row) return SDR_E_INVALID;
+    if (!o.in_path && o.row_stride < row) {
+        for (sdr_ctx* c : sh.ctx) sdr_ctx_destroy(c);
+        return SDR_E_INVALID;
+    }
     sh.nblocks_known = o.in_path ? regular_file_blocks(o.in_path, row * o.nch) : o.nblocks;
     // streams: the PLLs on [0, pll_cus) (halves), everything else on the rest
     const int half = o.pll_cus / 2;
