@@ -178,17 +178,23 @@ PLLM_HD Phase phase_detect(float eI, float eQ, double c, double s, double mr, in
 //  * phase_detect2: with (eI, eQ) = x * (RN c, -RN s), rotating by +t gives X = x (1 + delta),
 //    |delta| <= 2^-23, and Y = x c s (alpha + a - beta - b) for the four f32 rounding errors,
 //    so |Y / X| <= 2^-23 whenever |x| >= 2^-60 (subnormal products then only touch terms below
-//    2^-66). d = Y * rx replaces Y / X with an absolute error <= |d| (|delta| + 2^-51) < 2^-45.9,
-//    and atan2(eQ, eI) = base + d where base = -t + pi [x < 0] (mod 2pi) is prepared from the
-//    PREVIOUS step's quadrant before this step's input is touched (base_angle). EPS_ABS_E2 bounds
-//    the distance from e to the reference's f64 atan2: d's 2^-45.9, the kernels' 0.5 (eps_s +
-//    eps_c) < 2^-48.3, base's and the final add's roundings (2^-52 each), the representation of
-//    pi/2 times |m| <= 2 (2^-52.8), glibc atan2's own <= 1 ulp (2^-51): 2^-45.56 in all, under
-//    2^-45 (round 5; 2^-44 before, profiles/r05/: half the chunk redos). Measured:
-//    tools/pllmath/validate_e2.cpp, 2^-47.9 over 2e7 samples.
+//    2^-66). d = Y * rx replaces Y / X with an absolute error <= |Y/x| (|delta| + 2^-51).
+//    Bounded jointly (round 6): with p = a + alpha + a alpha, q = b + beta + b beta (|p|, |q| <=
+//    2u + u^2, u = 2^-24), Y/x = c s (p - q) + O(u^2) and delta = c^2 p + s^2 q + O(u^2), so
+//    |Y/x| |delta| <= sqrt(C (1 - C)) |p - q| |C p + (1 - C) q| with C = c^2, whose maximum over the
+//    box is (2u)^2 / 2 = 2^-47 (at p = -q, C = (1 + 1/sqrt 2) / 2; tests/test_pll_math.py checks it
+//    on a grid) -- not the 2^-45.9 of bounding |d| <= 2^-23 and |delta| <= 2^-23 separately, which
+//    cannot both be reached. atan2(eQ, eI) = base + d where base = -t + pi [x < 0] (mod 2pi) is
+//    prepared from the PREVIOUS step's quadrant before this step's input is touched (base_angle).
+//    EPS_ABS_E2 bounds the distance from e to the reference's f64 atan2: the substitution's 2^-47,
+//    the kernels' 0.5 (eps_s + eps_c) < 2^-48.3, Y's own roundings (the lane-pair form rounds both
+//    products, 2^-54 |x| each: 2^-53), base's and the final add's roundings (2^-52 each), the
+//    representation of pi/2 times |m| <= 2 (2^-52.8), glibc atan2's own <= 1 ulp (2^-51):
+//    2^-46.36 in all, under 2^-46 (round 6; 2^-45 in round 5, 2^-44 before: each halving halves the
+//    e-bracket chunk redos). Measured: tools/pllmath/validate_e2.cpp, 2^-47.8 over 2e7 samples.
 // ------------------------------------------------------------------------------------------
 constexpr double MAGIC = 6755399441055744.0;   // 1.5 * 2^52: fma(x, c, MAGIC) - MAGIC = rint(x c)
-constexpr double EPS_ABS_E2 = 0x1p-45;
+constexpr double EPS_ABS_E2 = 0x1p-46;
 
 PLLM_HD double pll_rx(float x) {
     const float ax = __builtin_fabs(x);

@@ -16,7 +16,7 @@ for f in sdr_kernels.hip sdr_frontend.hip sdr_pll.hip sdr_taps.cpp; do
     sdr_frontend.hip) extra="${FEFLAGS:-}";;
     sdr_pll.hip) extra="-fno-slp-vectorize ${PLLFLAGS--mllvm -amdgpu-sched-strategy=max-ilp}";;
   esac
-  /opt/rocm/bin/hipcc $common $extra "$@" -c -o $d/$f.o real-time-sdr_amd/csrc/$f & pids="$pids $!"
+  /opt/rocm/bin/hipcc $common $extra "$@" -c -o $d/$f.o ${SRC:-real-time-sdr_amd/csrc}/$f & pids="$pids $!"
 done
 for p in $pids; do wait $p; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -Wl,-soname,libsdr_amd.so -o build/variants/$name.so $d/*.o
