@@ -119,7 +119,10 @@ constexpr int FE_PF = 5;           // tap rows prefetched this many samples ahea
                                    // 2-8 and hand-issued batches measured, profiles/r02/fe_exact_ab.txt)
 // exact front end: outputs per lane (16 halves the occupancy: 1.54x slower, profiles/r04/ab_fe_r16.txt;
 // 12 or 16 with the next tile's window prefetched in registers: slower too, profiles/r04/ab_fe_v4.txt)
-constexpr int FE_R = 8;
+#ifndef SDR_FE_R
+#define SDR_FE_R 8
+#endif
+constexpr int FE_R = SDR_FE_R;
 // exact discriminator: 1 = reciprocal + Newton step with a tie proof (IEEE division as the fallback),
 // 0 = the IEEE f64 division on every output
 #ifndef SDR_FE_DISC
