@@ -191,7 +191,9 @@ PLLM_HD Phase phase_detect(float eI, float eQ, double c, double s, double mr, in
 //    products, 2^-54 |x| each: 2^-53), base's and the final add's roundings (2^-52 each), the
 //    representation of pi/2 times |m| <= 2 (2^-52.8), glibc atan2's own <= 1 ulp (2^-51):
 //    2^-46.36 in all, under 2^-46 (round 6; 2^-45 in round 5, 2^-44 before: each halving halves the
-//    e-bracket chunk redos). Measured: tools/pllmath/validate_e2.cpp, 2^-47.8 over 2e7 samples.
+//    e-bracket chunk redos). Measured on the shipped lane-pair step (tools/pllmath/validate_e3.cpp,
+//    sdr_pll.hip pll_step_split operation for operation): 2^-47.2 over 2e7 samples, no accepted
+//    rounding different from the reference's; the v2 detector (validate_e2.cpp) 2^-47.8.
 // ------------------------------------------------------------------------------------------
 constexpr double MAGIC = 6755399441055744.0;   // 1.5 * 2^52: fma(x, c, MAGIC) - MAGIC = rint(x c)
 constexpr double EPS_ABS_E2 = 0x1p-46;
