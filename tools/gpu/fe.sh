@@ -1,3 +1,4 @@
+# isolated front end (tools/bench_frontend.py, both numerics modes); PMC=1 adds a kernel trace and one SQ counter pass
 set -o pipefail
 export TMPDIR=/tmp
 timeout -k 10 300 python tools/bench_frontend.py > gpurun_out/fe.json 2> gpurun_out/fe.err; rc=$?

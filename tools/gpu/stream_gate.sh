@@ -1,3 +1,4 @@
+# kernel trace of tools/microbench/stream_gate.py (does a masked stream start work while another queue waits?)
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/gate
