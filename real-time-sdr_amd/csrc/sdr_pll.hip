@@ -440,38 +440,7 @@ struct SplitRegs {
     double toff;
     double mr;       // -r
     uint32_t nq1, b; // 1 - q, [r < 0]
-    uint32_t tlo, thi, tmask;   // SDR_PLL_BASETAB: the next step's base-angle table entry (prefetched)
-    uint32_t rhi;               // SDR_PLL_BASETAB: r's high word (its sign picks +-pi)
 };
-
-#ifndef SDR_PLL_BASETAB
-#define SDR_PLL_BASETAB 0
-#endif
-// Base angle from a 4-entry LDS table (SDR_PLL_BASETAB): base_angle_n's m is k - 1 for k = (nlo + nq1)
-// mod 4 < 3 and, for k = 3, +2 when r >= 0 and -2 when r < 0, so base = RN(T[k] + mr) with T[k] = m pi/2
-// (exact) and the sign of pi for k = 3 taken from r's sign bit by one v_bitop3: no b, no int -> f64
-// conversion, no fma (round 5 measured the form: 41.4 against 43.2 VALU per step, but its table read
-// was consumed five instructions after issue, 242 cycles per step). Here the entry of step j + 1 is
-// read during step j, right after its quadrant is known, and consumed after step j + 1's products.
-struct BaseTab {
-    uint32_t lo, hi, mask, pad;
-};
-__device__ __forceinline__ void base_tab_init(BaseTab* t) {
-    const double v[4] = {-pllm::PIO2, 0.0, pllm::PIO2, 2.0 * pllm::PIO2};
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint64_t u = __builtin_bit_cast(uint64_t, v[k]);
-        t[k] = BaseTab{(uint32_t)u, (uint32_t)(u >> 32), k == 3 ? 0x80000000u : 0u, 0u};
-    }
-}
-// the entry for a step whose rx has low word nlo, after the step with quadrant word nq1
-__device__ __forceinline__ void base_tab_fetch(SplitRegs& r, const BaseTab* t, uint32_t nlo) {
-    const uint32_t off = ((nlo + r.nq1) << 4) & 0x30u;   // v_add_lshl_u32 + v_and_b32
-    const BaseTab e = *reinterpret_cast<const BaseTab*>(reinterpret_cast<const char*>(t) + off);
-    r.tlo = e.lo;
-    r.thi = e.hi;
-    r.tmask = e.mask;
-}
 
 struct SplitLane {
     double c0, c1, c2, c3, c4, c5;   // P(z) = c0 + c1 z + ... + c5 z^5
@@ -506,7 +475,7 @@ __device__ __forceinline__ double pair_swap(double v) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ PllRegs split_to_full(const SplitRegs& s, bool a, bool bt = false) {
+__device__ __forceinline__ PllRegs split_to_full(const SplitRegs& s, bool a) {
     PllRegs r;
     const double fo = pair_swap(s.f);
     const float fbo = pair_swap(s.fb);
@@ -518,8 +487,7 @@ __device__ __forceinline__ PllRegs split_to_full(const SplitRegs& s, bool a, boo
     r.toff = s.toff;
     r.mr = s.mr;
     r.nq1 = s.nq1;
-    // the BT step keeps no b: [r < 0] is mr's sign bit clear (for every r, -0 included)
-    r.b = bt ? (uint32_t)(__builtin_bit_cast(uint64_t, s.mr) >> 63) ^ 1u : s.b;
+    r.b = s.b;
     return r;
 }
 
@@ -535,23 +503,13 @@ __device__ __forceinline__ SplitRegs full_to_split(const PllRegs& r, bool a) {
     return s;
 }
 
-template <bool TAB, bool BT = false>
+template <bool TAB>
 __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx, float Kp, float Ki, double w,
-                                               double wt, float& t_out, PllProof& pf, const SplitLane& L,
-                                               const BaseTab* btab = nullptr, uint32_t nlo_next = 0u) {
+                                               double wt, float& t_out, PllProof& pf, const SplitLane& L) {
     // pll.cpp:36-39 across the pair (see above)
     const float g = xs * pair_swap(r.fb);
     const double q = (double)g * r.f;
-    double base;
-    if constexpr (BT) {
-        uint32_t lo = r.tlo, hi = r.thi;
-        asm volatile("" : "+v"(lo), "+v"(hi) : "v"(q));   // consumed after the products (read a step ago)
-        uint32_t h;   // tmask ? rhi : hi, bitwise (truth table 0xAC)
-        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xac" : "=v"(h) : "v"(r.tmask), "v"(hi), "v"(r.rhi));
-        base = __builtin_bit_cast(double, ((uint64_t)h << 32) | lo) + r.mr;
-    } else {
-        base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
-    }
+    const double base = pllm::base_angle_n(pllm::lo_word(rx), r.nq1, r.b, r.mr);
     // (ed = base + rx qA + rx qB, own product first, is one dependent level shorter but needs both
     // bracket ends per lane: 2 instructions more, slower, profiles/r03/ab_pll_split.txt)
     const double Y = q + pair_swap(q);
@@ -578,15 +536,7 @@ __device__ __forceinline__ void pll_step_split(SplitRegs& r, float xs, double rx
     const double kdn = kdp - pllm::MAGIC1;
     const double rr = pllm::fma_(kdn, pllm::PIO2_LO, pllm::fma_(kdn, pllm::PIO2_HI, x));
     r.nq1 = (uint32_t)__builtin_bit_cast(uint64_t, kdp);
-    if constexpr (BT) {
-        base_tab_fetch(r, btab, nlo_next);      // read now, a step before its use
-        r.rhi = (uint32_t)(__builtin_bit_cast(uint64_t, rr) >> 32);
-#if SDR_PLL_BASETAB == 1
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-    } else {
-        r.b = (uint32_t)(__builtin_bit_cast(uint64_t, rr) >> 63);
-    }
+    r.b = (uint32_t)(__builtin_bit_cast(uint64_t, rr) >> 63);
     r.mr = -rr;
     const double z = rr * rr;
     const double u = pllm::fma_(rr, L.k1, L.k0);
@@ -693,17 +643,10 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
             }
         }
     };
-    constexpr bool BT = SDR_PLL_BASETAB != 0;
-    __shared__ BaseTab btab[4];
-    if (BT) base_tab_init(btab);   // every lane writes the same words: a wave's own writes precede its reads
     if (nmain > 0) {
         if (GATE) gate_wait(*gate, NB * C);
 #pragma unroll
         for (int u = 0; u < NB; u++) load_chunk(xb[u], rb[u], u * C);
-        if (BT) {
-            base_tab_fetch(r, btab, pllm::lo_word(rb[0][0]));
-            r.rhi = (uint32_t)(__builtin_bit_cast(uint64_t, -r.mr) >> 32);
-        }
     }
     for (int c0 = 0; c0 < nmain; c0 += NB) {
 #pragma unroll
@@ -722,8 +665,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
             float tv[C];
 #pragma unroll
             for (int j = 0; j < C; j++)
-                pll_step_split<TAB, BT>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf, L, btab,
-                                        pllm::lo_word(j + 1 < C ? rb[u][j + 1 < C ? j + 1 : 0] : rb[(u + 1) % NB][0]));
+                pll_step_split<TAB>(r, xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0, tv[j], pf, L);
             // this lane's proof: its half of the e bracket, the e range, its own rounding ties, and
             // the state range (a NaN from an invalid input fails it)
             const bool ok = (pf.emaxf < PLL_EMAX_F) & (pf.split == 0u) & (pf.tie > pllm::TIE_MIN) &
@@ -739,16 +681,12 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
             const int ok_partner = __builtin_amdgcn_mov_dpp((int)ok, 0xB1, 0xF, 0xF, false);
             const bool pair_ok = ok & (ok_partner != 0);
             if (!pair_ok) {
-                PllRegs full = split_to_full(snap, L.a, BT);
+                PllRegs full = split_to_full(snap, L.a);
 #pragma unroll
                 for (int j = 0; j < C; j++)
                     pll_step<true, TAB>(full, L.a ? -xb[u][j] : xb[u][j], rb[u][j], Kp, Ki, w, TAB ? wv[j] : 0.0,
                                         tv[j], pf);
                 r = full_to_split(full, L.a);
-                if (BT) {   // the next chunk's first step
-                    base_tab_fetch(r, btab, pllm::lo_word(rb[(u + 1) % NB][0]));
-                    r.rhi = (uint32_t)(__builtin_bit_cast(uint64_t, -r.mr) >> 32);
-                }
             }
             if (VEC) {
 #pragma unroll
@@ -762,7 +700,7 @@ __device__ __forceinline__ void pll_run_split(const PllJob& jb, int n, int ch, c
             load_chunk(xb[u], rb[u], min(c0 + u + NB, nmain - 1) * C);
         }
     }
-    PllRegs full = split_to_full(r, L.a, BT);
+    PllRegs full = split_to_full(r, L.a);
     {
         // the rest (< NB chunks + n % C steps): full checked steps on both lanes of the pair
         PllProof pf;
