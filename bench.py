@@ -229,6 +229,16 @@ class GpuStepper:
         # many sample ranges (sdr_frontend_pre_parts), so the PLL starts on its first range
         self.fill_parts = int(os.environ.get("SDR_BENCH_FILL_PARTS", "4"))
         self.parts_block = -1
+        # SDR_BENCH_FILL_NEXT (A/B): what the second block's front end waits for. "parts" (default,
+        # round 6): the first block's parts only (that block's mono stage runs on the all-CU stream
+        # after them); "mono" (round 5): the parts and then the mono stage on the front-end stream,
+        # ~70 us later. The PLL waited for the second block's input 0.17 ms per phase with "mono",
+        # 0.09 with "parts" (−0.4 % per step at equal shader clock, 3 interleaved triples,
+        # profiles/r06/fill_next/ab.txt). It cannot start before
+        # the parts: it continues their tails (the front end's I/Q tail and discriminator state, the
+        # FIRs' histories); "all": "parts", and the second block's front end and pre-PLL FIRs on the
+        # all-CU stream too
+        self.fill_next = os.environ.get("SDR_BENCH_FILL_NEXT", "parts")
         self.ev_fork, self.ev_join = torch.cuda.Event(), torch.cuda.Event()
         # SDR_BENCH_PLL=persistent (default): one PLL dispatch per phase (warm-up, timed) that waits
         # for each block's device flag (sdr_plls_launch/_signal/_wait); "dispatch": one sdr_plls
@@ -334,7 +344,8 @@ class GpuStepper:
         self.next_first = False
         if first:
             self.phase = (b, b + getattr(self, "phase_len", 1) - 1)
-        edge_fe = self.s_all is not None and b == self.phase[0]
+        edge_fe = self.s_all is not None and (
+            b == self.phase[0] or (self.fill_next == "all" and b == self.phase[0] + 1 == self.parts_block + 1))
         edge_post = self.s_all is not None and b == self.phase[1]
         if edge_fe:
             s_fe = self.s_all
@@ -363,11 +374,14 @@ class GpuStepper:
             if self.persist:                                  # stereo.cpp:77 + rds.cpp:119
                 pipe.plls_signal(stream=s_fe)
         self.pre_done[b].record(s_fe)
+        s_mono = s_fe
         if edge_fe:                                           # the rest of the phase's front ends follow it
             s_fe = self.s_fe
             s_fe.wait_event(self.pre_done[b])
-        pipe.mono(self.mono, stream=s_fe)                     # mono.cpp:34-42 (off the PLLs' critical path)
-        with torch.cuda.stream(s_fe):
+            if self.fill_next == "mono" or b != self.parts_block:
+                s_mono = s_fe
+        pipe.mono(self.mono, stream=s_mono)                   # mono.cpp:34-42 (off the PLLs' critical path)
+        with torch.cuda.stream(s_mono):
             torch.index_select(self.mono, 0, self.vsel, out=self.cap_mono[b])
         if self.persist:
             pipe.plls_wait(stream=s_post)
@@ -470,7 +484,8 @@ class GpuStepper:
                 # host-timed phase spends outside the span (pipeline fill before block 0's PLL and
                 # the last block's post stage after it)
                 span = (te[-1] - ts[0]) * 1e-5
-                idle = sum(max(0, ts[j] - te[j - 1]) for j in range(1, len(ts))) * 1e-5
+                gaps = [max(0, ts[j] - te[j - 1]) * 1e-2 for j in range(1, len(ts))]   # µs
+                idle = sum(gaps) * 1e-3
                 first, last = warmup, warmup + steps - 1
                 phase = self.fe_start[first].elapsed_time(self.post_done[last])
                 # drain: from the release of the PLL's last block (the post stream's wait) to the end
@@ -478,9 +493,12 @@ class GpuStepper:
                 # first block's front end and pre-PLL FIRs up to the PLL's first published range)
                 drain = self.pll_done[last].elapsed_time(self.post_done[last])
                 timeline = {"pll_span_ms": round(span, 4), "pll_idle_ms": round(idle, 4),
+                            "pll_idle_us_by_block": [round(g, 1) for g in gaps],
+                            "pll_block_us": [round((te[j] - ts[j]) * 1e-2, 1) for j in range(len(ts))],
                             "outside_span_ms": round(elapsed * 1e3 - span, 4),
                             "device_phase_ms": round(phase, 4), "fill_ms": round(phase - span - drain, 4),
                             "fill_parts": self.fill_parts if self.parts_block == first else 1,
+                            "fill_next": self.fill_next,
                             "drain_ms": round(drain, 4)}
                 sides = self._fe_vs_pll(ts, te)
                 if sides:

@@ -35,6 +35,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef SDR_FILL_FE_PARTS
+#define SDR_FILL_FE_PARTS 0      // sdr_frontend_pre_parts: one front-end launch per part (A/B only)
+#endif
+
 namespace sdrk {
 namespace {
 thread_local std::string g_err;
@@ -2753,12 +2757,17 @@ int sdr_frontend_pre_parts(sdr_ctx* c, const uint8_t* iq, size_t iq_stride, int 
     auto undo = [&](int r) { c->parity = parity0; c->block = block0; return r; };
     // part q: the FIR tiles [x0, x1) and the front-end tiles their windows need (tile j writes
     // outputs [adv j, adv j + adv), adv = 64 R - 1); after each part but the last, the count of
-    // published tiles
+    // published tiles. The front end runs in two launches (SDR_FILL_FE_PARTS 0): the first part's
+    // tiles, then all the rest with the second part -- one launch fills the chip where three part
+    // launches did not, so the block's front end ends ~0.1 ms earlier and the next block's (which
+    // continues its I/Q tail) can start (profiles/r06/fill_fe/ab.txt); SDR_FILL_FE_PARTS 1: one
+    // front-end launch per part (round 4)
     const int fe_adv = 64 * frontend_tab_r() - 1;
     int fe_done = 0;
     for (int q = 0; q < nparts; q++) {
         const int x0 = q * ntiles / nparts, x1 = (q + 1) * ntiles / nparts;
-        const int fe_end = q == nparts - 1 ? fe_tiles : std::min(fe_tiles, cdiv(std::min(x1 * FRB_TILE, n), fe_adv));
+        const bool fe_split = q < nparts - 1 && (SDR_FILL_FE_PARTS || q == 0);
+        const int fe_end = fe_split ? std::min(fe_tiles, cdiv(std::min(x1 * FRB_TILE, n), fe_adv)) : fe_tiles;
         int r = SDR_OK;
         if (fe_end > fe_done) r = frontend_launch(a, s, fe_done, fe_end - fe_done);
         fe_done = std::max(fe_done, fe_end);
