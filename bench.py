@@ -1254,13 +1254,16 @@ def queue_child(a) -> None:
     # run 1 (untimed, like the bench's warm-up): the checked captures, and the process's first use of
     # every kernel and buffer; run 2 (timed): the same blocks from fresh contexts, the same outputs
     run(True)
+    t_call = time.perf_counter()
     st = run(False)
+    call_s = time.perf_counter() - t_call          # the timed run's call: set-up + run + tear-down
     period_us = [[round(float(e[b] - e[b - 1]) / 100.0, 1) for b in range(1, nb)] for e in ends]
     np.savez(a.cap_out, lr=lr, nbits=nbits, bits=bits)
     import hashlib
     iq_sha = hashlib.sha256(np.ascontiguousarray(iq[:, ch].cpu().numpy()).tobytes()).hexdigest()
     print(json.dumps({"iq_sha": iq_sha, "pll_block_us": period_us, "blocks": st.blocks, "seconds": st.seconds, "steady_seconds": st.steady_seconds,
                       "pll_period_ms": st.pll_period_ms, "pll_span_ms": st.pll_span_ms, "d2h_ms": st.d2h_ms, "persistent": st.persistent,
+                      "call_s": call_s,
                       "block_iq": info.block_iq}), flush=True)
 
 

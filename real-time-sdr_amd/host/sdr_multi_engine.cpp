@@ -60,11 +60,45 @@ hipStream_t plain_stream() {
 }
 
 // a stream on CUs [first, first + n) (exclude = 0) or on every other CU (exclude = 1); its own
-// hardware queue (sdr_stream_create_cu_range)
+// hardware queue (sdr_stream_create_cu_range). Streams outlive a run, like the pinned buffers below:
+// making and destroying the six masked streams took ~30 + ~40 ms per run, in which the GPU idled
+// and its clock fell before the next run's first blocks (profiles/r06/queue_fill/). A run takes idle
+// pooled streams of its CU range; SDR_MULTI_STREAM_CACHE=0: made and destroyed per run.
+struct PooledStream {
+    int device, first, n, exclude;
+    void* s;
+};
+std::mutex g_stream_mu;
+std::vector<PooledStream> g_stream_free, g_stream_live;
+bool stream_cache_on() {
+    const char* e = std::getenv("SDR_MULTI_STREAM_CACHE");
+    return !e || std::atoi(e) != 0;
+}
 hipStream_t masked_stream(int device, int first, int n, int exclude) {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    for (size_t i = 0; i < g_stream_free.size(); i++) {
+        const PooledStream& p = g_stream_free[i];
+        if (p.device == device && p.first == first && p.n == n && p.exclude == exclude) {
+            g_stream_live.push_back(p);
+            g_stream_free.erase(g_stream_free.begin() + (long)i);
+            return (hipStream_t)g_stream_live.back().s;
+        }
+    }
     void* s = nullptr;
     check_sdr(sdr_stream_create_cu_range(&s, device, first, n, exclude), "sdr_stream_create_cu_range");
+    g_stream_live.push_back({device, first, n, exclude, s});
     return (hipStream_t)s;
+}
+// the end of a run: the stream (idle by then) back to the pool, or destroyed
+void release_masked(hipStream_t h) {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    for (size_t i = 0; i < g_stream_live.size(); i++)
+        if (g_stream_live[i].s == (void*)h) {
+            if (stream_cache_on()) g_stream_free.push_back(g_stream_live[i]);
+            else (void)sdr_stream_destroy(h);
+            g_stream_live.erase(g_stream_live.begin() + (long)i);
+            return;
+        }
 }
 
 hipEvent_t new_event() {
@@ -218,6 +252,12 @@ struct Shared {
     std::condition_variable start_cv;
     int ready = 0;
     bool go = false;
+    // the pipeline fill: block 1's front end is enqueued only after both consumers have ordered their
+    // block 1 pre parts behind block 0's (consumer_pll), so that it runs after block 0's pre parts
+    // instead of beside them -- those start the PLLs (SDR_MULTI_FILL=0: no such wait, round 6's first
+    // engine; profiles/r06/queue_fill/)
+    bool fill_gate = true;
+    int first_pre = 0;
     void arrive_and_wait() {
         (void)hipStreamQuery(s_fe);
         std::unique_lock<std::mutex> lk(start_mu);
@@ -330,6 +370,10 @@ void rf_thread(Shared* sh) {
             check_hip(hipStreamWaitEvent(s, h2d[k], 0), "hipStreamWaitEvent");
             src = d_iq[k];
         }
+        if (b == 1 && sh->s_all && sh->fill_gate) {   // after both consumers' block 0 pre parts (Shared)
+            std::unique_lock<std::mutex> lk(sh->start_mu);
+            sh->start_cv.wait(lk, [sh] { return sh->first_pre == 2; });
+        }
         if (b == 1) sh->t_block1 = std::chrono::steady_clock::now();
         const hipStream_t sf = fe_stream(sh, b);
         if (!dev_in && sf != s) check_hip(hipStreamWaitEvent(sf, h2d[(int)(b & 1)], 0), "hipStreamWaitEvent");
@@ -374,7 +418,12 @@ void consumer_pll(Shared* sh, sdr_ctx* ctx, int indicator, hipEvent_t pre, hipEv
     if (sh->persistent) {
         const hipStream_t sf = fe_stream(sh, b), sp = post_stream(sh, indicator, b);
         check_sdr(sdr_plls_signal(ctx, sf), "sdr_plls_signal");
-        if (sf != sh->s_fe) follow(sh->s_fe, sf, sh->ev_first[1 + indicator]);   // block 1's pre after block 0's
+        if (sf != sh->s_fe) {
+            follow(sh->s_fe, sf, sh->ev_first[1 + indicator]);   // block 1's pre after block 0's
+            std::lock_guard<std::mutex> lk(sh->start_mu);
+            sh->first_pre++;
+            sh->start_cv.notify_all();
+        }
         if (sp != sh->s_post_c[indicator]) follow(sp, sh->s_post_c[indicator], sh->ev_last[1 + indicator]);
         check_sdr(sdr_plls_wait(ctx, sp), "sdr_plls_wait");
         return;
@@ -518,6 +567,39 @@ void rds_thread(Shared* sh) {
         if (x) check_hip(hipStreamSynchronize(x), "hipStreamSynchronize");
 }
 
+// pinned host buffers outlive a run: a process that runs the receiver again (a server taking one input
+// after another, bench.py's timed second run) reuses them instead of pinning ~25 MB anew, which took
+// ~50 ms in which the GPU sat idle and its clock fell (profiles/r06/queue_fill/). Held until the
+// process exits; SDR_MULTI_PIN_CACHE=0: allocated and freed per run.
+std::mutex g_pin_mu;
+std::vector<std::pair<size_t, void*>> g_pin_free;
+bool pin_cache_on() {
+    const char* e = std::getenv("SDR_MULTI_PIN_CACHE");
+    return !e || std::atoi(e) != 0;
+}
+template <typename T>
+void pinned_get(T** p, size_t bytes) {
+    if (pin_cache_on()) {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        for (size_t i = 0; i < g_pin_free.size(); i++)
+            if (g_pin_free[i].first == bytes) {
+                *p = static_cast<T*>(g_pin_free[i].second);
+                g_pin_free.erase(g_pin_free.begin() + (long)i);
+                return;
+            }
+    }
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(p), bytes, hipHostMallocDefault), "hipHostMalloc");
+}
+void pinned_put(void* p, size_t bytes) {
+    if (!p) return;
+    if (!pin_cache_on()) {
+        (void)hipHostFree(p);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pin_free.emplace_back(bytes, p);
+}
+
 void alloc_consumers(Shared* sh) {
     const sdr_multi_opts& o = sh->o;
     AudioRes& a = sh->ar;
@@ -530,7 +612,7 @@ void alloc_consumers(Shared* sh) {
         a.out_ready[h] = new_event();
         a.d0[h] = timing_event();
         a.d1[h] = timing_event();
-        check_hip(hipHostMalloc(reinterpret_cast<void**>(&a.h_lr[h]), lr_bytes, hipHostMallocDefault), "hipHostMalloc");
+        pinned_get(&a.h_lr[h], lr_bytes);
     }
     RdsRes& r = sh->rr;
     r.pre = new_event();
@@ -539,19 +621,19 @@ void alloc_consumers(Shared* sh) {
     check_hip(hipMalloc(reinterpret_cast<void**>(&r.d_bits), (size_t)o.nch * SDR_MAX_BITS), "hipMalloc");
     for (int h = 0; h < NH; h++) {
         r.out_ready[h] = new_event();
-        check_hip(hipHostMalloc(reinterpret_cast<void**>(&r.h_nbits[h]), o.nch * sizeof(int32_t), hipHostMallocDefault),
-                  "hipHostMalloc");
-        check_hip(hipHostMalloc(reinterpret_cast<void**>(&r.h_bits[h]), (size_t)o.nch * SDR_MAX_BITS,
-                                hipHostMallocDefault), "hipHostMalloc");
+        pinned_get(&r.h_nbits[h], o.nch * sizeof(int32_t));
+        pinned_get(&r.h_bits[h], (size_t)o.nch * SDR_MAX_BITS);
     }
 }
 
 void free_consumers(Shared* sh) {
+    const sdr_multi_opts& o = sh->o;
     AudioRes& a = sh->ar;
+    const size_t lr_bytes = 2 * (size_t)sh->info.n_audio * o.nch * sizeof(int16_t);
     for (hipEvent_t e : {a.pre, a.pll, a.post}) (void)hipEventDestroy(e);
     for (int h = 0; h < NH; h++) {
         for (hipEvent_t e : {a.out_ready[h], a.d0[h], a.d1[h]}) (void)hipEventDestroy(e);
-        (void)hipHostFree(a.h_lr[h]);
+        pinned_put(a.h_lr[h], lr_bytes);
     }
     for (int k = 0; k < 2; k++) (void)hipFree(a.d_lr[k]);
     RdsRes& r = sh->rr;
@@ -560,17 +642,25 @@ void free_consumers(Shared* sh) {
     (void)hipFree(r.d_bits);
     for (int h = 0; h < NH; h++) {
         (void)hipEventDestroy(r.out_ready[h]);
-        (void)hipHostFree(r.h_nbits[h]);
-        (void)hipHostFree(r.h_bits[h]);
+        pinned_put(r.h_nbits[h], o.nch * sizeof(int32_t));
+        pinned_put(r.h_bits[h], (size_t)o.nch * SDR_MAX_BITS);
     }
 }
 
 // device-clock period per block of a finished persistent launch, blocks 1 .. last, and the span
 // from block 0's start to the last block's end (ms)
-void launch_period_ms(sdr_ctx* ctx, hipStream_t s, double* period, double* span, unsigned long long* ends, int nends) {
+void launch_period_ms(sdr_ctx* ctx, hipStream_t s, double* period, double* span, unsigned long long* ends, int nends,
+                      bool trace) {
     std::vector<unsigned long long> t0(65536), t1(65536);
     int nb = 0;
     check_sdr(sdr_plls_timeline(ctx, t0.data(), t1.data(), (int)t0.size(), &nb, s), "sdr_plls_timeline");
+    if (trace) {   // per block: the PLL's wait for its input (start - previous end) and its duration, us
+        std::fprintf(stderr, "sdr_multi: PLL idle/duration us:");
+        for (int b = 0; b < nb; b++)
+            std::fprintf(stderr, " %.0f/%.0f", b ? ((double)t0[(size_t)b] - (double)t1[(size_t)b - 1]) / 100.0 : 0.0,
+                         ((double)t1[(size_t)b] - (double)t0[(size_t)b]) / 100.0);
+        std::fprintf(stderr, "\n");
+    }
     if (ends)
         for (int b = 0; b < nends && b < nb; b++) ends[b] = t1[(size_t)b];
     if (nb < 2) return;
@@ -594,9 +684,18 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
     sh.o = *opts;
     const sdr_multi_opts& o = sh.o;
     check_hip(hipSetDevice(o.device), "hipSetDevice");
+    // SDR_MULTI_TRACE=1: the set-up and tear-down phases' host times on stderr
+    const bool trace = std::getenv("SDR_MULTI_TRACE") && std::atoi(std::getenv("SDR_MULTI_TRACE")) != 0;
+    const auto t_call = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (trace)
+            std::fprintf(stderr, "sdr_multi: %-16s %8.2f ms\n", what,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count());
+    };
     check_sdr(sdr_ctx_create(&sh.ctx[0], o.device, o.nch, o.mode, 0, o.flags), "sdr_ctx_create");
     check_sdr(sdr_ctx_create(&sh.ctx[1], o.device, o.nch, o.mode, 0, o.flags), "sdr_ctx_create");
     check_sdr(sdr_ctx_create(&sh.ctx[2], o.device, o.nch, o.mode, 1, o.flags), "sdr_ctx_create");
+    mark("contexts");
     check_sdr(sdr_ctx_info(sh.ctx[0], &sh.info), "sdr_ctx_info");
     const size_t row = 2 * (size_t)sh.info.block_iq;
     if (!o.in_path && o.row_stride < row) {
@@ -644,7 +743,9 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
     if (o.in_path) sh.s_copy = plain_stream();
     // SDR_MULTI_D2H=copy: the L/R copies on a stream of their own instead of after the post stages
     if (const char* e = std::getenv("SDR_MULTI_D2H"); e && std::strcmp(e, "copy") == 0) sh.s_d2h = plain_stream();
+    mark("streams");
     alloc_consumers(&sh);
+    mark("consumer buffers");
     // two recycled device batches of fm_demod [nch][block_if] (threadsafequeue.h's one slot, plus the
     // one the producer fills meanwhile)
     std::vector<FmBatch> batches(2);
@@ -661,12 +762,14 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
         sh.q.add_free(&fb);
     }
     check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    mark("batches");
     // one persistent launch per consumer for every block (before the first sdr_push_fm_demod)
     if (sh.persistent) {
         check_sdr(sdr_plls_launch_sel(sh.ctx[1], (int)sh.nblocks_known, SDR_PLLS_STEREO, sh.s_pll[0]), "sdr_plls_launch_sel");
         check_sdr(sdr_plls_launch_sel(sh.ctx[2], (int)sh.nblocks_known, SDR_PLLS_RDS, sh.s_pll[1]), "sdr_plls_launch_sel");
     }
     if (const char* e = std::getenv("SDR_MULTI_SYNC"); e && std::strcmp(e, "event") == 0) g_poll_events = false;
+    if (const char* e = std::getenv("SDR_MULTI_FILL"); e && std::atoi(e) == 0) sh.fill_gate = false;
     std::thread t_rds(rds_thread, &sh);      // project.cpp:134-136
     std::thread t_audio(audio_thread, &sh);
     std::thread t_rf(rf_thread, &sh);
@@ -675,6 +778,7 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
         std::unique_lock<std::mutex> lk(sh.start_mu);
         sh.start_cv.wait(lk, [&sh] { return sh.ready == 3; });
         t0 = std::chrono::steady_clock::now();
+        mark("threads ready");
         sh.go = true;
         sh.start_cv.notify_all();
     }
@@ -682,6 +786,7 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
     t_audio.join();
     t_rds.join();
     const auto t_end = std::chrono::steady_clock::now();
+    mark("run end");
     sdr_multi_stats st{};
     st.blocks = sh.blocks;
     st.seconds = std::chrono::duration<double>(t_end - t0).count();
@@ -697,7 +802,7 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
             int nb = 0;
             check_sdr(sdr_plls_report(sh.ctx[1 + i], ms, 0, &nb, sh.s_pll[i]), "sdr_plls_report");   // a timeout fails here
             launch_period_ms(sh.ctx[1 + i], sh.s_pll[i], &st.pll_period_ms, &st.pll_span_ms,
-                             o.pll_end ? o.pll_end + (size_t)i * o.stamp_blocks : nullptr, o.stamp_blocks);
+                             o.pll_end ? o.pll_end + (size_t)i * o.stamp_blocks : nullptr, o.stamp_blocks, trace);
         }
     }
     check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -709,16 +814,17 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
     free_consumers(&sh);
     for (sdr_ctx* c : sh.ctx) sdr_ctx_destroy(c);
     if (sh.s_d2h) (void)hipStreamDestroy(sh.s_d2h);
-    if (sh.s_post_c[1] != sh.s_post) (void)sdr_stream_destroy(sh.s_post_c[1]);
-    if (sh.s_all) (void)sdr_stream_destroy(sh.s_all);
+    if (sh.s_post_c[1] != sh.s_post) release_masked(sh.s_post_c[1]);
+    if (sh.s_all) release_masked(sh.s_all);
     for (int i = 0; i < 3; i++)
         for (hipEvent_t ev : {sh.ev_first[i], sh.ev_last[i]})
             if (ev) (void)hipEventDestroy(ev);
     for (hipStream_t s : {sh.s_fe, sh.s_post, sh.s_pll[0], sh.s_pll[1]}) {
-        if (half > 0) (void)sdr_stream_destroy(s);
+        if (half > 0) release_masked(s);
         else (void)hipStreamDestroy(s);
     }
     if (sh.s_copy) (void)hipStreamDestroy(sh.s_copy);
+    mark("torn down");
     if (stats) *stats = st;
     return SDR_OK;
 }
