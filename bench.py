@@ -495,6 +495,9 @@ class GpuStepper:
                 timeline = {"pll_span_ms": round(span, 4), "pll_idle_ms": round(idle, 4),
                             "pll_idle_us_by_block": [round(g, 1) for g in gaps],
                             "pll_block_us": [round((te[j] - ts[j]) * 1e-2, 1) for j in range(len(ts))],
+                            "pll_period_us": [round((te[j] - te[j - 1]) * 1e-2, 1) for j in range(1, len(te))],
+                            "pll_block_mhz": [round(m, 1) for m in self.pipe.plls_block_cycles(stream=self.s_pll)[1]],
+                            "pll_block_cycles": [round(c, 1) for c in self.pipe.plls_block_cycles(stream=self.s_pll)[0]],
                             "outside_span_ms": round(elapsed * 1e3 - span, 4),
                             "device_phase_ms": round(phase, 4), "fill_ms": round(phase - span - drain, 4),
                             "fill_parts": self.fill_parts if self.parts_block == first else 1,

@@ -249,6 +249,10 @@ int sdr_plls_timeline(sdr_ctx *ctx, unsigned long long *t_start, unsigned long l
  * and wave (s_memtime over each wave's compute of each block, averaged) and the shader clock over
  * the same intervals (against the 100 MHz s_memrealtime); synchronises `stream`. */
 int sdr_plls_cycles(sdr_ctx *ctx, double *cycles_per_step, double *clock_mhz, void *stream);
+/* The same per block j < max of the last persistent launch (cycles per step and wave, shader clock);
+ * *n = the launch's block count. */
+int sdr_plls_block_cycles(sdr_ctx *ctx, double *cycles_per_step, double *clock_mhz, int max, int *n,
+                          void *stream);
 /* rds symbol/bit recovery (rds.cpp:135-167): per channel, for blocks with block_count > 5 and
  * rds_on: offset = cdr(), symbols (0/1 bytes), bits (decoded 0/1 bytes). nbits[ch] = -1 on
  * blocks that do not decode. Any output pointer may be NULL. Strides in elements. */

@@ -107,6 +107,7 @@ def lib() -> C.CDLL:
         "sdr_plls_wait": ([vp, vp], i32),
         "sdr_plls_report": ([vp, C.POINTER(C.c_double), i32, C.POINTER(i32), vp], i32),
         "sdr_plls_cycles": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), vp], i32),
+        "sdr_plls_block_cycles": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), i32, C.POINTER(C.c_int), vp], i32),
         "sdr_plls_timeline": ([vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), i32, C.POINTER(i32), vp], i32),
         "sdr_rds_post": ([vp, vp, sz, vp], i32),
         "sdr_ctx_buffer": ([vp, C.c_char_p, C.POINTER(vp), C.POINTER(sz), C.POINTER(i32)], i32),
@@ -408,6 +409,15 @@ class Pipeline:
         cyc, mhz = C.c_double(0.0), C.c_double(0.0)
         check(lib().sdr_plls_cycles(self._h, C.byref(cyc), C.byref(mhz), _stream(stream)), "sdr_plls_cycles")
         return cyc.value, mhz.value
+
+    def plls_block_cycles(self, stream=None, max_blocks: int = 4096) -> tuple[list, list]:
+        """Per block of the last persistent launch: (cycles per step and wave, shader clock MHz)."""
+        cyc, mhz = (C.c_double * max_blocks)(), (C.c_double * max_blocks)()
+        n = C.c_int(0)
+        check(lib().sdr_plls_block_cycles(self._h, cyc, mhz, max_blocks, C.byref(n), _stream(stream)),
+              "sdr_plls_block_cycles")
+        k = min(n.value, max_blocks)
+        return list(cyc[:k]), list(mhz[:k])
 
     def rds_post(self, out=None, bits=True, stream=None, bits_out=None):
         """bits_out: a [nch][SDR_MAX_BITS] u8 tensor the block's bits go to instead of self.bits."""

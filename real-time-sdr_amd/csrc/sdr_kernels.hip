@@ -2879,6 +2879,22 @@ int sdr_plls_cycles(sdr_ctx* c, double* cycles_per_step, double* clock_mhz, void
     return SDR_OK;
 }
 
+int sdr_plls_block_cycles(sdr_ctx* c, double* cycles_per_step, double* clock_mhz, int max, int* n_out, void* stream) {
+    if (!c || !c->pers_cyc || c->pers_last_n <= 0) return fail(SDR_E_INVALID, "plls_block_cycles: no persistent launch");
+    hipStream_t s = S(stream);
+    const int n = c->pers_last_n;
+    std::vector<unsigned long long> v((size_t)2 * n);
+    HIP_TRY(hipMemcpyAsync(v.data(), c->pers_cyc, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const double steps = (double)c->pers_waves * c->info.block_if;
+    for (int j = 0; j < n && j < max; j++) {
+        if (cycles_per_step) cycles_per_step[j] = steps > 0 ? (double)v[2 * j] / steps : -1.0;
+        if (clock_mhz) clock_mhz[j] = v[2 * j + 1] ? (double)v[2 * j] / (double)v[2 * j + 1] * 100.0 : -1.0;
+    }
+    if (n_out) *n_out = n;
+    return SDR_OK;
+}
+
 int sdr_rds_post(sdr_ctx* c, float* rds_clean, size_t rds_stride, void* stream) {
     if (!c) return fail(SDR_E_INVALID, "null context");
     if (const int rf_ = check_failed(c, "rds_post")) return rf_;
