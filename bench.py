@@ -1242,11 +1242,14 @@ def queue_child(a) -> None:
     cap_ch = (C.c_int * nv)(*ch)
     ends = np.zeros((2, nb), np.uint64)
 
-    def run(capture: bool) -> "Stats":
+    lr2, nbits2, bits2 = np.zeros_like(lr), np.zeros_like(nbits), np.zeros_like(bits)
+
+    def run(cap) -> "Stats":
+        c_lr, c_nbits, c_bits = cap
         o = Opts(nch=a.channels, mode=0, flags=0, device=0, pll_cus=a.cus, in_path=None, d_iq=iq.data_ptr(),
                  row_stride=iq.stride(1), block_stride=iq.stride(0), nblocks=nb, out_prefix=None,
-                 ncap=nv if capture else 0, cap_blocks=nb, cap_ch=cap_ch, cap_lr=lr.ctypes.data if capture else None,
-                 cap_nbits=nbits.ctypes.data if capture else None, cap_bits=bits.ctypes.data if capture else None,
+                 ncap=nv, cap_blocks=nb, cap_ch=cap_ch, cap_lr=c_lr.ctypes.data,
+                 cap_nbits=c_nbits.ctypes.data, cap_bits=c_bits.ctypes.data,
                  stamp_blocks=nb, pll_end=ends.ctypes.data)
         st = Stats()
         torch.cuda.synchronize(dev)
@@ -1255,18 +1258,26 @@ def queue_child(a) -> None:
             raise SystemExit(f"sdr_multi_run: {rc} {pkg.lib().sdr_last_error()}")
         return st
     # run 1 (untimed, like the bench's warm-up): the checked captures, and the process's first use of
-    # every kernel and buffer; run 2 (timed): the same blocks from fresh contexts, the same outputs
-    run(True)
+    # every kernel and buffer; run 2 (timed): the same blocks from the initial state again (the
+    # engine's pooled contexts, reset), its captures compared with run 1's
+    run((lr, nbits, bits))
     t_call = time.perf_counter()
-    st = run(False)
+    st = run((lr2, nbits2, bits2))
     call_s = time.perf_counter() - t_call          # the timed run's call: set-up + run + tear-down
+    timed_equal = bool(np.array_equal(lr, lr2) and np.array_equal(nbits, nbits2))
+    for b, j in np.argwhere(nbits > 0) if timed_equal else ():        # the bits a row holds
+        k = int(nbits[b, j])
+        timed_equal = timed_equal and np.array_equal(bits[b, j, :k], bits2[b, j, :k])
+    if not timed_equal:
+        print(f"queue child: timed run differs: lr {np.array_equal(lr, lr2)} nbits {np.array_equal(nbits, nbits2)}",
+              file=sys.stderr)
     period_us = [[round(float(e[b] - e[b - 1]) / 100.0, 1) for b in range(1, nb)] for e in ends]
     np.savez(a.cap_out, lr=lr, nbits=nbits, bits=bits)
     import hashlib
     iq_sha = hashlib.sha256(np.ascontiguousarray(iq[:, ch].cpu().numpy()).tobytes()).hexdigest()
     print(json.dumps({"iq_sha": iq_sha, "pll_block_us": period_us, "blocks": st.blocks, "seconds": st.seconds, "steady_seconds": st.steady_seconds,
                       "pll_period_ms": st.pll_period_ms, "pll_span_ms": st.pll_span_ms, "d2h_ms": st.d2h_ms, "persistent": st.persistent,
-                      "call_s": call_s,
+                      "call_s": call_s, "timed_run_equal": timed_equal,
                       "block_iq": info.block_iq}), flush=True)
 
 
@@ -1316,6 +1327,7 @@ def queue_plumbed_leg(args, st, nch: int) -> dict:
         "pll": "persistent" if q["persistent"] else "per-block dispatch",
         "d2h_ms": round(q["d2h_ms"], 2),
         "outputs_equal_to_bench_capture": bool(equal),
+        "timed_run_outputs_equal": q.get("timed_run_equal"),
         "checked_channels": cap["channels"],
     }
     return res

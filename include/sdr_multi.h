@@ -63,9 +63,10 @@ typedef struct sdr_multi_stats {
  * started). Once its threads run, a failure -- an unreadable input or output file, a library or HIP
  * runtime error, a persistent PLL launch that timed out -- prints "sdr: <what>" on stderr and ends the
  * process with exit(1), as the reference program does (rffrontend.cpp:50-52, utilities.h:7-10): the
- * three stage threads cannot be unwound from each other's queue waits. The run's CU-masked streams and
- * pinned output buffers are kept for the process's later runs (a run reuses idle ones of the same CU
- * range and size; SDR_MULTI_STREAM_CACHE=0 / SDR_MULTI_PIN_CACHE=0: made and freed per run). */
+ * three stage threads cannot be unwound from each other's queue waits. The run's contexts, CU-masked
+ * streams and pinned output buffers are kept for the process's later runs (a run reuses idle ones of
+ * the same shape, contexts through sdr_ctx_reset; SDR_MULTI_CTX_CACHE=0 / SDR_MULTI_STREAM_CACHE=0 /
+ * SDR_MULTI_PIN_CACHE=0: made and freed per run). */
 int sdr_multi_run(const sdr_multi_opts *opts, sdr_multi_stats *stats);
 
 #ifdef __cplusplus

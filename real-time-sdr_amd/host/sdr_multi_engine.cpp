@@ -101,6 +101,48 @@ void release_masked(hipStream_t h) {
         }
 }
 
+// contexts outlive a run too (SDR_MULTI_CTX_CACHE=0: made and destroyed per run): a later run with
+// the same channels, mode and flags takes an idle one back to the reference's initial state
+// (sdr_ctx_reset) in ~1 ms instead of ~3 ms to make and ~10 ms to destroy, with the GPU idle meanwhile
+struct PooledCtx {
+    int device, nch, mode, rds_on, flags;
+    sdr_ctx* c;
+};
+std::mutex g_ctx_mu;
+std::vector<PooledCtx> g_ctx_free;
+std::vector<PooledCtx> g_ctx_live;
+bool ctx_cache_on() {
+    const char* e = std::getenv("SDR_MULTI_CTX_CACHE");
+    return !e || std::atoi(e) != 0;
+}
+sdr_ctx* ctx_get(int device, int nch, int mode, int rds_on, int flags) {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    for (size_t i = 0; i < g_ctx_free.size(); i++) {
+        const PooledCtx& p = g_ctx_free[i];
+        if (p.device == device && p.nch == nch && p.mode == mode && p.rds_on == rds_on && p.flags == flags) {
+            check_sdr(sdr_ctx_reset(p.c, nullptr), "sdr_ctx_reset");
+            g_ctx_live.push_back(p);
+            g_ctx_free.erase(g_ctx_free.begin() + (long)i);
+            return g_ctx_live.back().c;
+        }
+    }
+    sdr_ctx* c = nullptr;
+    check_sdr(sdr_ctx_create(&c, device, nch, mode, rds_on, flags), "sdr_ctx_create");
+    g_ctx_live.push_back({device, nch, mode, rds_on, flags, c});
+    return c;
+}
+void ctx_put(sdr_ctx* c) {   // after the run's streams have drained
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    for (size_t i = 0; i < g_ctx_live.size(); i++)
+        if (g_ctx_live[i].c == c) {
+            if (ctx_cache_on()) g_ctx_free.push_back(g_ctx_live[i]);
+            else sdr_ctx_destroy(c);
+            g_ctx_live.erase(g_ctx_live.begin() + (long)i);
+            return;
+        }
+    sdr_ctx_destroy(c);
+}
+
 hipEvent_t new_event() {
     hipEvent_t e = nullptr;
     check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
@@ -692,14 +734,14 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
             std::fprintf(stderr, "sdr_multi: %-16s %8.2f ms\n", what,
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count());
     };
-    check_sdr(sdr_ctx_create(&sh.ctx[0], o.device, o.nch, o.mode, 0, o.flags), "sdr_ctx_create");
-    check_sdr(sdr_ctx_create(&sh.ctx[1], o.device, o.nch, o.mode, 0, o.flags), "sdr_ctx_create");
-    check_sdr(sdr_ctx_create(&sh.ctx[2], o.device, o.nch, o.mode, 1, o.flags), "sdr_ctx_create");
+    sh.ctx[0] = ctx_get(o.device, o.nch, o.mode, 0, o.flags);
+    sh.ctx[1] = ctx_get(o.device, o.nch, o.mode, 0, o.flags);
+    sh.ctx[2] = ctx_get(o.device, o.nch, o.mode, 1, o.flags);
     mark("contexts");
     check_sdr(sdr_ctx_info(sh.ctx[0], &sh.info), "sdr_ctx_info");
     const size_t row = 2 * (size_t)sh.info.block_iq;
     if (!o.in_path && o.row_stride < row) {
-        for (sdr_ctx* c : sh.ctx) sdr_ctx_destroy(c);
+        for (sdr_ctx* c : sh.ctx) ctx_put(c);
         return SDR_E_INVALID;
     }
     sh.nblocks_known = o.in_path ? regular_file_blocks(o.in_path, row * o.nch) : o.nblocks;
@@ -812,7 +854,7 @@ extern "C" int sdr_multi_run(const sdr_multi_opts* opts, sdr_multi_stats* stats)
         for (auto& e : fb.released) (void)hipEventDestroy(e);
     }
     free_consumers(&sh);
-    for (sdr_ctx* c : sh.ctx) sdr_ctx_destroy(c);
+    for (sdr_ctx* c : sh.ctx) ctx_put(c);
     if (sh.s_d2h) (void)hipStreamDestroy(sh.s_d2h);
     if (sh.s_post_c[1] != sh.s_post) release_masked(sh.s_post_c[1]);
     if (sh.s_all) release_masked(sh.s_all);
