@@ -1217,6 +1217,9 @@ def _multi_structs():
     return Opts, Stats
 
 
+QUEUE_WARM_BLOCKS = 40    # untimed blocks before the queue child's timed run
+
+
 def queue_child(a) -> None:
     """bench.py --queue-child: the multi-channel receiver engine (include/sdr_multi.h: the reference's
     three stage threads joined by ThreadSafeQueue<FmBatch*>, threadsafequeue.h:24-74) over the bench's
@@ -1258,9 +1261,13 @@ def queue_child(a) -> None:
             raise SystemExit(f"sdr_multi_run: {rc} {pkg.lib().sdr_last_error()}")
         return st
     # run 1 (untimed, like the bench's warm-up): the checked captures, and the process's first use of
-    # every kernel and buffer; run 2 (timed): the same blocks from the initial state again (the
-    # engine's pooled contexts, reset), its captures compared with run 1's
+    # every kernel and buffer; more untimed runs up to 40 warm-up blocks in all (bench.py's default
+    # warm-up; the child starts on a GPU idle since the bench's CPU legs); the timed run: the same
+    # blocks from the initial state again (the engine's pooled contexts, reset), its captures compared
+    # with run 1's
     run((lr, nbits, bits))
+    for _ in range(1, -(-QUEUE_WARM_BLOCKS // nb)):
+        run((lr2, nbits2, bits2))
     t_call = time.perf_counter()
     st = run((lr2, nbits2, bits2))
     call_s = time.perf_counter() - t_call          # the timed run's call: set-up + run + tear-down
@@ -1317,8 +1324,9 @@ def queue_plumbed_leg(args, st, nch: int) -> dict:
                    "fm_demod batches, one context per thread, each consumer's PLL as its own persistent launch "
                    "(sdr_plls_launch_sel), L/R PCM and RDS bits copied to the host every block",
         "input": f"the bench's device-generated input, same channels and blocks ({q['blocks']} blocks incl. the "
-                 f"warm-up), regenerated in a child process; timed: the second of two runs over those blocks from "
-                 f"fresh contexts (the first, untimed like the bench's warm-up, gives the checked captures)",
+                 f"warm-up), regenerated in a child process; timed: a run over those blocks after untimed runs of "
+                 f">= {QUEUE_WARM_BLOCKS} blocks in all (the first gives the checked captures), from the "
+                 f"initial state (pooled contexts reset), its outputs equal to the first run's",
         "value": round(q["blocks"] * samples / q["seconds"] / 1e6, 2), "unit": "MS/s",
         "ms_per_block": round(q["seconds"] / q["blocks"] * 1e3, 4),
         "pll_period_value": (round(samples / (q["pll_period_ms"] * 1e-3) / 1e6, 2) if q["pll_period_ms"] else None),
