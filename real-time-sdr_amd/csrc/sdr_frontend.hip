@@ -420,99 +420,6 @@ __device__ __forceinline__ void fe_fir(const uint8_t* __restrict__ sw, const flo
     }
 }
 
-// The same sweep with the tap rows fetched in groups of G samples (SDR_FE_TAPS): the compiler's
-// own tap loads above must wait with lgkmcnt(0) before every use of a row (scalar loads return out
-// of order), and it places that wait after the loads it has just issued for later rows and after
-// the next LDS chunk read -- the wave stalls for their whole latency about every fourth sample.
-// Here the rows of group g+1 are issued at the start of group g and waited for at its end, after G
-// samples of multiplies, and the LDS chunk reads a group needs are issued at its start; the wait
-// (hand-issued, tied to the loaded registers) is the only one on the taps. R = 8: a row is 8 taps,
-// one s_load_dwordx8.
-#ifndef SDR_FE_TAPS
-#define SDR_FE_TAPS 0
-#endif
-#ifndef SDR_FE_TG
-#define SDR_FE_TG 3
-#endif
-typedef float fe_f8v __attribute__((ext_vector_type(8)));
-template <int D, int G>
-__device__ __forceinline__ void fe_fir_g(const uint8_t* __restrict__ sw, const float* __restrict__ hs, f32x2 (&acc)[8]) {
-    constexpr int R = 8, NT = 101, HP = NT - 1;
-    constexpr int TWIN = (R - 1) * D + NT;
-    constexpr int TCH = (2 * TWIN + 15) / 16;
-    constexpr int NG = (TWIN + G - 1) / G;
-    const int t = threadIdx.x;
-    uint4 chunk[TCH];
-    const uint4* tw = reinterpret_cast<const uint4*>(sw + 2 * t * R * D);
-    chunk[TCH - 1] = tw[TCH - 1];
-    if (TCH >= 2) chunk[TCH - 2] = tw[TCH - 2];
-#pragma unroll
-    for (int r = 0; r < R; r++) acc[r] = f32x2{0.0f, 0.0f};
-    const uint64_t hsa = (uint64_t)(uintptr_t)hs;   // wave-uniform (a kernel argument): the loads' SGPR base
-    const float* hsu = reinterpret_cast<const float*>(
-        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)hsa) |
-        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(hsa >> 32)) << 32));
-    fe_f8v tb[2][G];
-    auto load_group = [&](fe_f8v (&d)[G], int g) {
-#pragma unroll
-        for (int j = 0; j < G; j++) {
-            const int S = TWIN - 1 - g * G - j;
-            if (S >= 0)
-                asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(d[j]) : "s"(hsu), "s"(S * R * 4) : "memory");
-        }
-    };
-    auto wait_group = [&](fe_f8v (&d)[G]) {
-        // the wait redefines the loaded registers, so no use of them is scheduled above it
-        if constexpr (G == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(d[0]) :: "memory");
-        if constexpr (G == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(d[0]), "+s"(d[1]) :: "memory");
-        if constexpr (G == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(d[0]), "+s"(d[1]), "+s"(d[2]) :: "memory");
-        if constexpr (G == 4)
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(d[0]), "+s"(d[1]), "+s"(d[2]), "+s"(d[3]) :: "memory");
-    };
-    auto sample = [&](int S) -> f32x2 {
-        const uint4 c4 = chunk[S >> 3];
-        const int dw = (S & 7) >> 1;
-        const uint32_t w = dw == 0 ? c4.x : dw == 1 ? c4.y : dw == 2 ? c4.z : c4.w;
-        return (S & 1) ? fe_cvt_v<1>(w) : fe_cvt_v<0>(w);
-    };
-    load_group(tb[0], 0);
-    wait_group(tb[0]);
-    f32x2 m_next = sample(TWIN - 1);
-#pragma unroll
-    for (int g = 0; g < NG; g++) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (g + 1 < NG) load_group(tb[(g + 1) & 1], g + 1);
-#pragma unroll
-        for (int j = 0; j < G; j++) {   // the LDS chunks this group's samples read two chunks ahead
-            const int S = TWIN - 1 - g * G - j;
-            if (S >= 0 && ((S & 7) == 7 || S == TWIN - 1) && (S >> 3) >= 2) chunk[(S >> 3) - 2] = tw[(S >> 3) - 2];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < G; j++) {
-            const int S = TWIN - 1 - g * G - j;
-            if (S < 0) break;
-            const fe_f8v& row = tb[g & 1][j];
-            const f32x2 m = m_next;
-            f32x2 prod[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int k = r * D + HP - S;
-                const double hp = __builtin_bit_cast(double, f32x2{row[(r >> 1) * 2], row[(r >> 1) * 2 + 1]});
-                if (k >= 0 && k < NT) prod[r] = fe_mul_v(hp, r & 1, m);
-            }
-            if (S > 0) m_next = sample(S - 1);
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int k = r * D + HP - S;
-                if (k >= 0 && k < NT) acc[r] = fe_add_v(acc[r], prod[r]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (g + 1 < NG) wait_group(tb[(g + 1) & 1]);
-    }
-}
-
 // The discriminator (demod.cpp:8-19) of lane t's R outputs c0 + t R + r and their stores into out
 // (fm_demod of the channel; c0 is the tile's carry output, never written); the block's last (I, Q)
 // goes to prev_out.
@@ -685,8 +592,7 @@ __global__ __launch_bounds__(64) void k_frontend2(
     }
     __syncthreads();
     f32x2 acc[R];
-    if constexpr (SDR_FE_TAPS && R == 8) fe_fir_g<D, SDR_FE_TG>(sw, hs, acc);
-    else fe_fir<R, D>(sw, hs, acc);
+    fe_fir<R, D>(sw, hs, acc);
     fe_disc_store<R>(acc, c0, ch, prev_in, prev_out, fm + (size_t)ch * fm_stride, block_if);
     float* out = fm + (size_t)ch * fm_stride;
     if (j == 0) {
