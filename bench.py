@@ -875,6 +875,8 @@ def run_rank(args, world: int, rank: int, local: int, stepper_factory=None, back
             st.prepare_phase(args.steps)
         win = LaunchWindow(torch, dist, win_dev, pending).arm()
         st.synchronize()
+        if os.environ.get("SDR_BENCH_IDLE_MS"):   # diagnosis: the GPU idle before the timer (profiles/r06/idle_gap)
+            time.sleep(float(os.environ["SDR_BENCH_IDLE_MS"]) / 1e3)
         t0 = time.perf_counter()
         with win:
             if hasattr(st, "begin_phase"):
