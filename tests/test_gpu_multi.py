@@ -65,7 +65,9 @@ def test_sdr_multi_file_to_pcm_and_rds(multi_input, multi_ref, tmp_path, source)
 def test_sdr_multi_run_device_input_captures(pkg, tmp_path):
     """sdr_multi_run over blocks resident on the device, as bench.py's queue_plumbed leg runs it (its
     child mode: the bench's generator, 8 distinct channels x 12 blocks): the captured stereo rows and
-    RDS bits of three channels equal the oracle's on the same input bytes, block for block."""
+    RDS bits of three channels equal the oracle's on the same input bytes, block for block, and the
+    timed run -- on the engine's pooled contexts (sdr_ctx_reset), streams and pinned buffers, after
+    the warm-up runs -- reproduces the first run's rows."""
     import hashlib
     import sys
     import torch
@@ -79,6 +81,7 @@ def test_sdr_multi_run_device_input_captures(pkg, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     q = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert q["blocks"] == nb and q["persistent"] == 1 and q["pll_period_ms"] > 0
+    assert q["timed_run_equal"] is True
     iq = bench.make_input(torch, nch, nb, first_channel=0, device=torch.device("cuda", 0))[:, ch].cpu().numpy()
     assert hashlib.sha256(np.ascontiguousarray(iq).tobytes()).hexdigest() == q["iq_sha"]
     got = np.load(out)
